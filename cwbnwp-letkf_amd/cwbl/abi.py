@@ -1,0 +1,271 @@
+"""ctypes mirror of include/cwb_letkf_core.h and a thin host wrapper.
+
+This is the Python-side binding a maintainer would use in place of the Fortran
+`bind(C)` interface (cwbnwp-letkf_amd/fortran/letkf_core_gpu.f90).  Struct layouts must
+match the header exactly; tests/test_abi.py checks sizes and offsets against the C
+compiler.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+ABI_VERSION = 1
+MAX_NVAR = 5
+NUM_GTS_TYPES = 29
+NUM_RADAR_TYPES = 4
+MAX_MEMBERS = 64
+
+GTS_SOUND, GTS_SYNOP, GTS_GPSPW, GTS_METAR, GTS_SHIPS = 1, 2, 8, 10, 11
+RADAR_DBZ, RADAR_VR, RADAR_ZDR, RADAR_KDP = 1, 2, 3, 4
+MEM_HOST, MEM_DEVICE = 0, 1
+Q1_REPLICATE, Q1_PER_TYPE = 0, 1
+
+#: obs variables per GTS type, in the order letkf_yoyb builds is_assim/err_muti
+#: (module_letkf_core.f90:349-417)
+GTS_NVAR = {GTS_SOUND: 4, GTS_SYNOP: 5, GTS_GPSPW: 1, GTS_METAR: 5, GTS_SHIPS: 5}
+
+ERRORS = {1: "CWBL_ERR_ARG", 2: "CWBL_ERR_STATE", 3: "CWBL_ERR_NO_DEVICE", 4: "CWBL_ERR_HIP",
+          5: "CWBL_ERR_UNSUPPORTED", 6: "CWBL_ERR_OOM"}
+
+
+class InitParams(C.Structure):
+    _fields_ = [("nmember", C.c_int), ("device", C.c_int), ("weight_function", C.c_int),
+                ("norain_value", C.c_float), ("q1_mode", C.c_int), ("reserved", C.c_int),
+                ("workspace_bytes", C.c_size_t)]
+
+
+class GtsObs(C.Structure):
+    _fields_ = [("type_id", C.c_int), ("nvar", C.c_int), ("nobs", C.c_int),
+                ("reserved", C.c_int), ("xyz", C.c_void_p), ("obs", C.c_void_p),
+                ("error", C.c_void_p), ("hdxb", C.c_void_p), ("qc", C.c_void_p)]
+
+
+class RadarObs(C.Structure):
+    _fields_ = [("type_id", C.c_int), ("nobs", C.c_int), ("xyz", C.c_void_p),
+                ("obs", C.c_void_p), ("hdxb", C.c_void_p)]
+
+
+class ObsSet(C.Structure):
+    _fields_ = [("n_gts", C.c_int), ("n_radar", C.c_int), ("gts", C.POINTER(GtsObs)),
+                ("radar", C.POINTER(RadarObs)), ("memory", C.c_int), ("reserved", C.c_int)]
+
+
+class TypeParams(C.Structure):
+    _fields_ = [("use_it", C.c_int), ("max_lz_pts", C.c_int), ("hclr", C.c_float),
+                ("vclr", C.c_float), ("err_muti", C.c_float * MAX_NVAR),
+                ("err_rej", C.c_float * MAX_NVAR), ("is_assim", C.c_int * MAX_NVAR)]
+
+
+class VarParams(C.Structure):
+    _fields_ = [("multi_infl", C.c_float), ("use_rtpp", C.c_int), ("rtpp_alpha", C.c_float),
+                ("use_rtps", C.c_int), ("rtps_alpha", C.c_float), ("reserved", C.c_int),
+                ("gts", TypeParams * NUM_GTS_TYPES), ("radar", TypeParams * NUM_RADAR_TYPES)]
+
+
+class Slab(C.Structure):
+    _fields_ = [("nx", C.c_int), ("ny", C.c_int), ("nz", C.c_int), ("alt_nx", C.c_int),
+                ("alt_ny", C.c_int), ("ix_lim", C.c_int), ("iy_lim", C.c_int),
+                ("memory", C.c_int), ("x", C.c_void_p), ("y", C.c_void_p),
+                ("alt", C.c_void_p), ("var", C.c_void_p)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("points", C.c_longlong), ("solved", C.c_longlong), ("nobs_sum", C.c_longlong),
+                ("lz_truncated", C.c_longlong), ("nonconverged", C.c_longlong),
+                ("q1_undefined", C.c_longlong), ("max_p", C.c_int), ("max_sweeps", C.c_int),
+                ("ntrees", C.c_int), ("reserved", C.c_int), ("ms_total", C.c_double),
+                ("ms_prep", C.c_double), ("ms_search", C.c_double), ("ms_solve", C.c_double),
+                ("ms_copy", C.c_double)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+
+
+#: exported symbols of the product library (include/cwb_letkf_core.h)
+EXPORTS = ["cwbl_init", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch", "cwbl_search",
+           "cwbl_finalize", "cwbl_last_error", "cwbl_abi_version"]
+
+
+def _ptr(a):
+    """Address of a host numpy array, a device tensor (anything with data_ptr()), or int."""
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return a
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+def _f4(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _i4(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+class ObsSetBuilder:
+    """Assemble a cwbl_obs_set from per-type arrays (host numpy or device tensors).
+
+    GTS arrays use the reference's Fortran layouts expressed as C-order numpy shapes:
+      xyz (nobs,3), obs/error (nobs,nvar), hdxb/qc (k,nobs,nvar)
+    radar: xyz (nobs,3), obs (nobs,), hdxb (k,nobs).
+    """
+
+    def __init__(self, memory=MEM_HOST):
+        self.memory = memory
+        self.gts, self.radar, self._keep = [], [], []
+
+    def _hold(self, a, conv):
+        if self.memory == MEM_HOST:
+            a = conv(a)
+        self._keep.append(a)
+        return _ptr(a)
+
+    def add_gts(self, type_id, xyz, obs, error, hdxb, qc):
+        nobs = int(xyz.shape[0])
+        nvar = int(obs.shape[1]) if nobs else GTS_NVAR[type_id]
+        g = GtsObs(type_id, nvar, nobs, 0, self._hold(xyz, _f4), self._hold(obs, _f4),
+                   self._hold(error, _f4), self._hold(hdxb, _f4), self._hold(qc, _i4))
+        self.gts.append(g)
+        return self
+
+    def add_radar(self, type_id, xyz, obs, hdxb):
+        nobs = int(xyz.shape[0])
+        r = RadarObs(type_id, nobs, self._hold(xyz, _f4), self._hold(obs, _f4),
+                     self._hold(hdxb, _f4))
+        self.radar.append(r)
+        return self
+
+    def build(self):
+        ga = (GtsObs * max(1, len(self.gts)))(*self.gts)
+        ra = (RadarObs * max(1, len(self.radar)))(*self.radar)
+        s = ObsSet(len(self.gts), len(self.radar), ga, ra, self.memory, 0)
+        s._keep = (ga, ra, self._keep)
+        return s
+
+
+def type_params(use_it=1, max_lz_pts=500, hclr=-1.0, vclr=-1.0, err_muti=1.0, err_rej=5.0,
+                is_assim=0):
+    """gts_config / radar_variable_config defaults follow module_config.f90:7-34."""
+    def five(v, ct):
+        v = list(v) if isinstance(v, (list, tuple, np.ndarray)) else [v] * MAX_NVAR
+        v = v + [v[-1]] * (MAX_NVAR - len(v))
+        return (ct * MAX_NVAR)(*v[:MAX_NVAR])
+    return TypeParams(int(use_it), int(max_lz_pts), float(hclr), float(vclr),
+                      five(err_muti, C.c_float), five(err_rej, C.c_float),
+                      five([int(x) for x in (is_assim if isinstance(is_assim, (list, tuple, np.ndarray)) else [is_assim])], C.c_int))
+
+
+def var_params(multi_infl=1.0, use_rtpp=0, rtpp_alpha=0.85, use_rtps=0, rtps_alpha=0.85,
+               gts=None, radar=None):
+    """inflation_nml defaults (module_config.f90:312-317); gts/radar: {type_id: TypeParams}."""
+    vp = VarParams()
+    vp.multi_infl, vp.use_rtpp, vp.rtpp_alpha = multi_infl, int(use_rtpp), rtpp_alpha
+    vp.use_rtps, vp.rtps_alpha = int(use_rtps), rtps_alpha
+    for i in range(NUM_GTS_TYPES):
+        vp.gts[i] = type_params(use_it=0)
+    for i in range(NUM_RADAR_TYPES):
+        vp.radar[i] = type_params(use_it=0)
+    for tid, tp in (gts or {}).items():
+        vp.gts[tid - 1] = tp
+    for tid, tp in (radar or {}).items():
+        vp.radar[tid - 1] = tp
+    return vp
+
+
+def make_slab(x, y, alt, var, ix_lim=None, iy_lim=None, memory=MEM_HOST):
+    """x,y: (ny,nx); alt: (nz,alt_ny,alt_nx); var: (k,nz,ny,nx) C-order == Fortran
+    var(nx,ny,nz,0:k-1).  Host arrays must be float32 C-contiguous (var is updated in place)."""
+    k, nz, ny, nx = var.shape
+    _, alt_ny, alt_nx = alt.shape
+    s = Slab(nx, ny, nz, alt_nx, alt_ny, ix_lim if ix_lim is not None else min(nx, alt_nx),
+             iy_lim if iy_lim is not None else min(ny, alt_ny), memory,
+             _ptr(x), _ptr(y), _ptr(alt), _ptr(var))
+    s._keep = (x, y, alt, var)
+    return s
+
+
+def default_library_path():
+    here = os.path.dirname(os.path.abspath(__file__))
+    return os.path.join(os.path.dirname(here), "lib", "libcwbl.so")
+
+
+def load_library(path=None):
+    """Load the product library; raises OSError when it has not been built."""
+    lib = C.CDLL(path or os.environ.get("CWBL_LIBRARY") or default_library_path())
+    vp, cp = C.c_void_p, C.c_char_p
+    lib.cwbl_init.argtypes = [C.POINTER(InitParams)]
+    lib.cwbl_set_obs.argtypes = [C.POINTER(ObsSet)]
+    lib.cwbl_analyze_var.argtypes = [C.POINTER(VarParams), C.POINTER(Slab), C.POINTER(Stats)]
+    lib.cwbl_solve_batch.argtypes = [C.c_int, vp, vp, vp, vp, C.c_float, C.c_int, C.c_float,
+                                     C.c_int, C.c_float, vp, vp, C.c_int]
+    lib.cwbl_search.argtypes = [C.c_int, vp, C.c_float, C.c_float, C.c_int, C.c_int, vp, vp,
+                                vp, vp, C.c_int]
+    lib.cwbl_finalize.argtypes = []
+    lib.cwbl_last_error.restype = cp
+    lib.cwbl_abi_version.restype = C.c_int
+    for fn in ("cwbl_init", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch",
+               "cwbl_search", "cwbl_finalize"):
+        getattr(lib, fn).restype = C.c_int
+    return lib
+
+
+class CwblError(RuntimeError):
+    pass
+
+
+class Core:
+    """Host wrapper over the C ABI (one per process; the library state is global like the
+    reference's module state)."""
+
+    def __init__(self, nmember, device=-1, weight_function=0, norain_value=-5.0,
+                 q1_mode=Q1_REPLICATE, workspace_bytes=0, lib=None):
+        self.lib = lib or load_library()
+        if self.lib.cwbl_abi_version() != ABI_VERSION:
+            raise CwblError("ABI version mismatch")
+        self.k = nmember
+        self._check(self.lib.cwbl_init(C.byref(InitParams(
+            nmember, device, weight_function, norain_value, q1_mode, 0, workspace_bytes))))
+
+    def _check(self, rc):
+        if rc != 0:
+            msg = self.lib.cwbl_last_error()
+            raise CwblError(f"{ERRORS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+    def set_obs(self, obs_set):
+        self._check(self.lib.cwbl_set_obs(C.byref(obs_set)))
+
+    def analyze_var(self, vp, slab):
+        st = Stats()
+        self._check(self.lib.cwbl_analyze_var(C.byref(vp), C.byref(slab), C.byref(st)))
+        return st
+
+    def solve_batch(self, col_off, yo, yb, xb, inflat, use_rtpp, rtpp_alpha, use_rtps,
+                    rtps_alpha, want_evals=False, memory=MEM_HOST, xa=None, evals=None):
+        npts = int(len(col_off) - 1)
+        if memory == MEM_HOST:
+            col_off = np.ascontiguousarray(col_off, np.int64)
+            yo, yb, xb = _f4(yo), _f4(yb), _f4(xb)
+            xa = np.empty((npts, self.k), np.float32)
+            evals = np.empty((npts, self.k), np.float64) if want_evals else None
+        self._check(self.lib.cwbl_solve_batch(
+            npts, _ptr(col_off), _ptr(yo), _ptr(yb), _ptr(xb), inflat, int(use_rtpp),
+            rtpp_alpha, int(use_rtps), rtps_alpha, _ptr(xa), _ptr(evals), memory))
+        return xa, evals
+
+    def search(self, obs_xyz, hclr, vclr, max_lz_pts, q_xyz):
+        obs_xyz, q_xyz = _f4(obs_xyz), _f4(q_xyz)
+        nq = q_xyz.shape[0]
+        nf = np.empty(nq, np.int32)
+        idx = np.empty((nq, max_lz_pts), np.int32)
+        r2 = np.empty((nq, max_lz_pts), np.float32)
+        self._check(self.lib.cwbl_search(obs_xyz.shape[0], _ptr(obs_xyz), hclr, vclr,
+                                         max_lz_pts, nq, _ptr(q_xyz), _ptr(nf), _ptr(idx),
+                                         _ptr(r2), MEM_HOST))
+        return nf, idx, r2
+
+    def finalize(self):
+        self._check(self.lib.cwbl_finalize())

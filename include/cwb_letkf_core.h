@@ -1,0 +1,209 @@
+/*
+ * cwb_letkf_core.h — C ABI of the MI355X LETKF analysis core.
+ *
+ * This is the drop-in boundary for the per-variable hot loop of the reference
+ * LETKF (lopunch/CWBNWP-LETKF).  A Fortran host binds it with iso_c_binding
+ * (see cwbnwp-letkf_amd/fortran/letkf_core_gpu.f90 and INTEGRATION.md); Python
+ * binds it with ctypes (cwbnwp-letkf_amd/cwbl/abi.py).
+ *
+ * Entry point                reference interface it replaces
+ * -------------------------  ------------------------------------------------------------
+ * cwbl_init                  set_optimal_workspace_for_eigen + set_ensemble_constants
+ *                            (module_eigen.f90:16-35, module_param.f90:241-247,
+ *                            called at cwb_letkf.f90:37-38)
+ * cwbl_set_obs               the obs state after gts%distribute / rad%distribute
+ *                            (module_gts_omboma.f90:508-611, module_radar.f90:120-186),
+ *                            i.e. wrfda_gts%platform(:) and cwb_radar%radarobs(:)
+ * cwbl_analyze_var           one pass of letkf_driver's update loop for one variable:
+ *                            build_tree x2 (module_letkf_core.f90:63-64) + the grid-point
+ *                            loop (module_letkf_core.f90:209-240) + destroy_tree (:295)
+ * cwbl_solve_batch           letkf_solve (module_letkf_core.f90:598-700) for many points
+ *                            with pre-assembled yo/yb (KAT / diagnostics entry)
+ * cwbl_search                build_tree + get_lz for one obs type
+ *                            (module_localization.f90:35-167, 188-331) (KAT entry)
+ * cwbl_finalize              destroy_eigen_array (module_eigen.f90:110-113)
+ * cwbl_last_error            replaces `stop "<msg>"`: the library never exits
+ *
+ * Conventions
+ *  - float <-> real(c_float), double <-> real(c_double), int <-> integer(c_int),
+ *    long long <-> integer(c_long_long).  Fortran logicals cross as int 0/1.
+ *  - Arrays are passed in the reference's Fortran (column-major) layout, first index
+ *    fastest; the comment next to each pointer gives the Fortran shape.
+ *  - Observation / result indices are 0-based on this side of the ABI.
+ *  - All calls are synchronous, from one host thread per process; `memory` says whether
+ *    the array pointers of a struct are host pointers (copied in/out inside the call) or
+ *    HIP device pointers already resident on the library's device.
+ *  - Return value 0 = success; nonzero = error code, message in cwbl_last_error().
+ *  - There is no CPU fallback: without a usable gfx950 device every compute entry point
+ *    returns CWBL_ERR_NO_DEVICE.
+ */
+#ifndef CWB_LETKF_CORE_H
+#define CWB_LETKF_CORE_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CWBL_ABI_VERSION 1
+
+#define CWBL_MAX_NVAR        5   /* obs variables per GTS report (u,v,t,p,q) */
+#define CWBL_NUM_GTS_TYPES  29   /* module_param.f90:172 num_gts_indexes     */
+#define CWBL_NUM_RADAR_TYPES 4   /* module_param.f90:212 num_radar_indexes   */
+#define CWBL_MAX_MEMBERS    64   /* k supported by the v1 solve kernels      */
+
+/* GTS type ids (module_param.f90:143-171); only these five are assimilated
+ * (module_localization.f90:59-72). */
+enum {
+  CWBL_GTS_SOUND = 1, CWBL_GTS_SYNOP = 2, CWBL_GTS_GPSPW = 8,
+  CWBL_GTS_METAR = 10, CWBL_GTS_SHIPS = 11
+};
+/* radar type ids (module_param.f90:208-211) */
+enum { CWBL_RADAR_DBZ = 1, CWBL_RADAR_VR = 2, CWBL_RADAR_ZDR = 3, CWBL_RADAR_KDP = 4 };
+
+enum { CWBL_MEM_HOST = 0, CWBL_MEM_DEVICE = 1 };
+
+enum {
+  CWBL_OK = 0,
+  CWBL_ERR_ARG = 1,          /* invalid argument / shape                        */
+  CWBL_ERR_STATE = 2,        /* call order (e.g. analyze before init/set_obs)    */
+  CWBL_ERR_NO_DEVICE = 3,    /* no HIP device / wrong architecture              */
+  CWBL_ERR_HIP = 4,          /* HIP runtime error                               */
+  CWBL_ERR_UNSUPPORTED = 5,  /* configuration outside v1 (e.g. k > 64)          */
+  CWBL_ERR_OOM = 6
+};
+
+/* Q1: build_tree picks the tree dimension from the last type appended
+ * (module_localization.f90:151).  CWBL_Q1_REPLICATE follows it wherever the result is
+ * defined (a 3-D type in a 2-D tree family is searched in 2-D); a 2-D type in a 3-D
+ * family reads an undefined qv(3) in the reference, and is searched in 2-D with its own
+ * tree (counted in cwbl_stats.q1_undefined).  CWBL_Q1_PER_TYPE uses every type's own
+ * vclr for its tree. */
+enum { CWBL_Q1_REPLICATE = 0, CWBL_Q1_PER_TYPE = 1 };
+
+typedef struct cwbl_init_params {
+  int    nmember;          /* k = config%nmember (module_config.f90:306), 2..64 */
+  int    device;           /* HIP device ordinal, -1 = current device */
+  int    weight_function;  /* 0 Gaussian, 1 Gaspari-Cohn (module_config.f90:307) */
+  float  norain_value;     /* control_nml norain_value (module_config.f90:295) */
+  int    q1_mode;          /* CWBL_Q1_* */
+  int    reserved;
+  size_t workspace_bytes;  /* device workspace budget for neighbour lists (0 = 2 GiB) */
+} cwbl_init_params;
+
+/* One GTS platform: type(gts_structure), module_gts_omboma.f90:13-22. */
+typedef struct cwbl_gts_obs {
+  int          type_id;   /* CWBL_GTS_* */
+  int          nvar;      /* 5 synop/metar/ships, 4 sound, 1 gpspw */
+  int          nobs;
+  int          reserved;
+  const float *xyz;       /* xyz(3,nobs), projected metres (module_param.f90:7) */
+  const float *obs;       /* obs(nvar,nobs) */
+  const float *error;     /* error(nvar,nobs) */
+  const float *hdxb;      /* hdxb(nvar,nobs,0:k-1) = H(x_b) per member (:171) */
+  const int   *qc;        /* qc(nvar,nobs,0:k-1) */
+} cwbl_gts_obs;
+
+/* One radar variable: type(radar_structure), module_radar.f90:13-16. */
+typedef struct cwbl_radar_obs {
+  int          type_id;   /* CWBL_RADAR_* */
+  int          nobs;
+  const float *xyz;       /* xyz(3,nobs), metres */
+  const float *obs;       /* obs(nobs) */
+  const float *hdxb;      /* hdxb(nobs,0:k-1) */
+} cwbl_radar_obs;
+
+typedef struct cwbl_obs_set {
+  int                   n_gts;
+  int                   n_radar;
+  const cwbl_gts_obs   *gts;     /* at most one entry per type id */
+  const cwbl_radar_obs *radar;
+  int                   memory;  /* CWBL_MEM_HOST / CWBL_MEM_DEVICE for the arrays */
+  int                   reserved;
+} cwbl_obs_set;
+
+/* Namelist values of one obs type for the current variable (index ivar of the
+ * per-variable arrays): gts_config / radar_variable_config, module_config.f90:7-34. */
+typedef struct cwbl_type_params {
+  int   use_it;                    /* %use_it */
+  int   max_lz_pts;                /* %max_lz_pts */
+  float hclr;                      /* %hclr(ivar) in km; <= 0 disables the type */
+  float vclr;                      /* %vclr(ivar) in km; <= 0 = no vertical localization */
+  float err_muti[CWBL_MAX_NVAR];   /* GTS: per obs variable %u..%q%err_muti; radar: [0] = %error */
+  float err_rej[CWBL_MAX_NVAR];    /* GTS: per obs variable; radar: [0] = %err_rej */
+  int   is_assim[CWBL_MAX_NVAR];   /* GTS: %u..%q%is_assim(ivar); radar: unused (hclr>0) */
+} cwbl_type_params;
+
+typedef struct cwbl_var_params {
+  float multi_infl;      /* inflation_nml multi_infl(ivar): inflat=(k-1)/multi_infl (:68) */
+  int   use_rtpp;
+  float rtpp_alpha;
+  int   use_rtps;
+  float rtps_alpha;
+  int   reserved;
+  cwbl_type_params gts[CWBL_NUM_GTS_TYPES];     /* index = gts type id - 1 */
+  cwbl_type_params radar[CWBL_NUM_RADAR_TYPES]; /* index = radar type id - 1 */
+} cwbl_var_params;
+
+/* One variable's local slab, exactly as letkf_driver holds it (module_letkf_core.f90:85,
+ * 171-172, 192-193): var(nx,ny,nz,0:k-1), lat/lon -> x/y(nx,ny), alt(alt_nx,alt_ny,nz). */
+typedef struct cwbl_slab {
+  int          nx, ny, nz;      /* leading dims of var and x/y */
+  int          alt_nx, alt_ny;  /* leading dims of alt (cpu%loc_nx, cpu%loc_ny) */
+  int          ix_lim, iy_lim;  /* analysed columns: i < ix_lim, j < iy_lim (:209-210, Q2) */
+  int          memory;          /* CWBL_MEM_HOST / CWBL_MEM_DEVICE */
+  const float *x;               /* proj%lonlat_to_xy(lon,lat)(1) per column, (nx,ny) */
+  const float *y;               /* ... (2) */
+  const float *alt;             /* alt(alt_nx,alt_ny,nz) metres */
+  float       *var;             /* in/out var(nx,ny,nz,0:k-1) */
+} cwbl_slab;
+
+typedef struct cwbl_stats {
+  long long points;          /* grid points visited (ix_lim*iy_lim*nz) */
+  long long solved;          /* points with >= 1 accepted obs (letkf_solve called) */
+  long long nobs_sum;        /* sum of p over solved points */
+  long long lz_truncated;    /* (point, type) searches that hit max_lz_pts (Q4) */
+  long long nonconverged;    /* eigensolves that hit the sweep cap (LAPACK info ignored, */
+                             /* module_eigen.f90:49) */
+  long long q1_undefined;    /* (point, type) searches in the Q1 undefined case */
+  int       max_p;           /* max p over points */
+  int       max_sweeps;      /* max Jacobi sweeps used */
+  int       ntrees;          /* trees built for this variable */
+  int       reserved;
+  double    ms_total;        /* wall time of the call */
+  double    ms_prep;         /* tree build + obs QC tables */
+  double    ms_search;       /* neighbour search kernels */
+  double    ms_solve;        /* solve kernels */
+  double    ms_copy;         /* host<->device copies of the slab (host memory only) */
+} cwbl_stats;
+
+int         cwbl_init(const cwbl_init_params *params);
+int         cwbl_set_obs(const cwbl_obs_set *obs);
+int         cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *slab,
+                             cwbl_stats *stats /* nullable */);
+
+/* letkf_solve for npts points.  Point i uses columns [col_off[i], col_off[i+1]) of
+ * yo(ncol) and yb(k,ncol) (member fastest), xb(k,npts) -> xa(k,npts).  evals (nullable)
+ * receives the eigenvalues of inflat*I + yb yb^T per point, ascending (k,npts). */
+int         cwbl_solve_batch(int npts, const long long *col_off, const float *yo,
+                             const float *yb, const float *xb, float inflat,
+                             int use_rtpp, float rtpp_alpha, int use_rtps, float rtps_alpha,
+                             float *xa, double *evals, int memory);
+
+/* build_tree + get_lz for one obs type: obs_xyz(3,nobs) metres, hclr/vclr km
+ * (vclr <= 0: 2-D), queries q_xyz(3,nq).  nfound(nq); idx/r2 (max_lz_pts,nq) in the
+ * reference's traversal order (0-based obs indices). */
+int         cwbl_search(int nobs, const float *obs_xyz, float hclr, float vclr,
+                        int max_lz_pts, int nq, const float *q_xyz,
+                        int *nfound, int *idx, float *r2, int memory);
+
+int         cwbl_finalize(void);
+const char *cwbl_last_error(void);
+int         cwbl_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CWB_LETKF_CORE_H */

@@ -1,0 +1,61 @@
+#!/bin/bash
+# Build oracle/_ref/ref_harness from the reference sources where they lie.
+#
+# TEST INFRASTRUCTURE ONLY.  Compiles, unmodified apart from the reference Makefile's own
+# preprocessing (`cpp -C -P -traditional ... -DREAL64`, Makefile:4,9,66-67):
+#   module_param.f90, module_config.f90, module_eigen.f90, module_kdtree2.f90
+# and the source text of
+#   letkf_solve        (module_letkf_core.f90:598-700)
+#   Gaspari_Cohn_1999  (module_localization.f90:333-364)
+# cut out at build time into a wrapper module (their home modules cannot be compiled here:
+# module_letkf_core/module_localization `use` grid/gts_omboma/radar, whose chain needs the
+# NetCDF-Fortran library and an MPI Fortran module, neither of which exists for amdflang in
+# this image — see DESIGN.md "Oracle").  Intermediate sources live in a temp dir that is
+# deleted; only the executable is written to oracle/_ref/.
+#
+# LAPACK/BLAS: MKL (libmkl_rt from /opt/conda/lib), sequential, MKL_CBWR=COMPATIBLE at run
+# time (the reference production build links Fujitsu SSL2, Makefile:11).
+set -euo pipefail
+REF=${REF:-/root/reference}
+HERE=$(cd "$(dirname "$0")" && pwd)
+OUT=$(cd "$HERE/.." && pwd)/_ref
+FC=${FC:-amdflang}
+MKLDIR=${MKLDIR:-/opt/conda/lib}
+
+if [ ! -d "$REF" ]; then echo "build_ref: $REF not present, skipping"; exit 0; fi
+command -v "$FC" >/dev/null || { echo "build_ref: $FC not found"; exit 1; }
+[ -e "$MKLDIR/libmkl_rt.so" ] || { echo "build_ref: MKL not found in $MKLDIR"; exit 1; }
+
+mkdir -p "$OUT"
+TMP=$(mktemp -d)
+trap 'rm -rf "$TMP"' EXIT
+CPP="cpp -C -P -traditional -Wno-invalid-pp-token -ffreestanding -DREAL64"
+
+for f in module_param module_config module_eigen module_kdtree2; do
+  $CPP "$REF/$f.f90" > "$TMP/$f.F90"
+done
+{
+  echo "module ref_extract"
+  echo "    use param"
+  echo "    use config"
+  echo "    use eigen"
+  echo "    implicit none"
+  echo "contains"
+  awk '/^    function letkf_solve\(/,/end function letkf_solve/' "$REF/module_letkf_core.f90"
+  awk '/pure function Gaspari_Cohn_1999\(/,/end function Gaspari_Cohn_1999/' "$REF/module_localization.f90"
+  echo "end module ref_extract"
+} > "$TMP/ref_extract.f90"
+grep -q "end function letkf_solve" "$TMP/ref_extract.f90"
+grep -q "end function Gaspari_Cohn_1999" "$TMP/ref_extract.f90"
+$CPP "$TMP/ref_extract.f90" > "$TMP/ref_extract.F90"
+
+cd "$TMP"
+FFLAGS="-O2"
+for f in module_param module_config module_eigen module_kdtree2 ref_extract; do
+  $FC $FFLAGS -c "$f.F90"
+done
+$FC $FFLAGS -I"$HERE" -c "$HERE/ref_harness.f90"
+$FC $FFLAGS -o "$OUT/ref_harness" module_param.o module_config.o module_eigen.o \
+  module_kdtree2.o ref_extract.o ref_harness.o \
+  -L"$MKLDIR" -lmkl_rt -Wl,-rpath,"$MKLDIR"
+echo "build_ref: built $OUT/ref_harness"
