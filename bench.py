@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X LETKF analysis core on BASELINE.json's headline metric.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+
+A "step" is one cwbl_analyze_var call on the configuration's full synthetic grid, i.e. one
+pass of the reference's per-variable hot loop (module_letkf_core.f90:63-64 + 209-240):
+k-d tree builds, QC columns, neighbour search and the per-point LETKF solve for every grid
+point.  Inputs (obs set and slab) are resident in HBM before the timed region.
+
+Multi-GPU (launched by torch.distributed.run, one process per GPU): grid rows are dealt
+cyclically to ranks (block-1 decomposition as in module_mpi_util.f90:73-188); the observation
+set is generated on rank 0 and sent to every rank with ONE RCCL broadcast (backend "nccl")
+before the timed region; there is no collective on the data path.  The grid is fixed as N
+grows (configs[2]: the 300x300x50 grid sharded across GPUs), so scaling is "strong".
+
+Rank 0 prints one JSON line.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "cwbnwp-letkf_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from cwbl import abi, synth  # noqa: E402
+
+METRIC = "analysis grid-points/sec (+ wall-clock per cycle) at k=40, 1/2/4/8 MI355X"
+FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector = matrix on gfx950), spec
+
+
+def cpu_baseline(w, target_s=12.0):
+    """Oracle (C restatement, OpenMP over host cores) on a bounded sample of the same
+    workload: a block of whole columns cut out of the grid.  Rank 0, N=1 only."""
+    from helpers import oracle
+    lib = oracle()
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+
+    def run(nb):
+        j0, i0 = w.ny // 2 - nb // 2, w.nx // 2 - nb // 2
+        sub = lambda a: np.ascontiguousarray(a[..., j0:j0 + nb, i0:i0 + nb])  # noqa: E731
+        var = sub(w.var).copy()
+        slab = abi.make_slab(sub(w.x), sub(w.y), sub(w.alt), var)
+        st = abi.Stats()
+        t0 = time.perf_counter()
+        rc = lib.orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp), C.byref(slab),
+                                 threads, C.byref(st))
+        dt = time.perf_counter() - t0
+        assert rc == 0
+        return dt, st, nb * nb * w.nz
+
+    dt, st, pts = run(4)
+    rate = pts / dt
+    nb = int(max(4, min(w.nx, np.sqrt(target_s * rate / w.nz))))
+    dt, st, pts = run(nb)
+    return {"value": pts / dt, "unit": "grid-points/s", "cores": threads, "kind": "port",
+            "sample": f"{nb}x{nb} columns x {w.nz} levels = {pts} points of the {w.name} grid "
+                      f"({dt:.1f} s), mean p={st.nobs_sum / max(st.solved, 1):.0f}, "
+                      f"LAPACK={lib.orc_lapack_name().decode()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    w = synth.make(args.config, rows=(rank, world) if world > 1 else None)
+    k = w.k
+    # ---- observation set: generated on rank 0, one RCCL broadcast --------------------------
+    n = w.obs.shape[0]
+    pack = torch.empty(n * (4 + k), dtype=torch.float32, device=dev)
+    if rank == 0:
+        pack.copy_(torch.from_numpy(np.concatenate([w.obs_xyz.ravel(), w.obs, w.hdxb.ravel()])))
+    bcast_ms = 0.0
+    if world > 1:
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        dist.broadcast(pack, src=0)
+        torch.cuda.synchronize()
+        bcast_ms = (time.perf_counter() - t0) * 1e3
+    oxyz = pack[:3 * n].view(n, 3)
+    oobs = pack[3 * n:4 * n]
+    ohdxb = pack[4 * n:].view(k, n)
+    # ---- slab in HBM ---------------------------------------------------------------------------
+    x, y, alt = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt))
+    var = torch.from_numpy(w.var).to(dev)
+    torch.cuda.synchronize()
+
+    core = abi.Core(k, device=local)
+    core.set_obs(abi.ObsSetBuilder(abi.MEM_DEVICE).add_radar(w.radar_type, oxyz, oobs, ohdxb).build())
+    slab = abi.make_slab(x, y, alt, var, memory=abi.MEM_DEVICE)
+
+    for _ in range(args.warmup):
+        core.analyze_var(w.vp, slab)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        stats.append(core.analyze_var(w.vp, slab))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    pts_local = sum(s.points for s in stats)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        p = torch.tensor([pts_local], dtype=torch.float64, device=dev)
+        dist.all_reduce(p, op=dist.ReduceOp.SUM)
+        elapsed, pts_total = float(t.item()), float(p.item())
+    else:
+        pts_total = float(pts_local)
+
+    if rank == 0:
+        solved = sum(s.solved for s in stats)
+        nobs_sum = sum(s.nobs_sum for s in stats)
+        ms_solve = sum(s.ms_solve for s in stats)
+        ms_search = sum(s.ms_search for s in stats)
+        flops = synth.flops_total(k, solved, nobs_sum)
+        achieved = flops / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else 0.0
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "pmc_solve_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        out = {
+            "metric": METRIC,
+            "value": pts_total / elapsed,
+            "unit": "grid-points/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.config}: {w.nx}x{w.extra['cfg']['ny']}x{w.nz} grid, k={k}, "
+                            f"{n} radar-VR-like obs (hclr {w.extra['cfg']['hclr']} km, vclr "
+                            f"{w.extra['cfg']['vclr']} km), RTPP+RTPS, Gaussian localisation",
+                "grid_points": int(w.extra["cfg"]["nx"] * w.extra["cfg"]["ny"] * w.nz),
+                "k": k,
+                "n_obs": n,
+                "mean_p": nobs_sum / max(solved, 1),
+                "parallelism": f"column-sharded x{world}" + (", RCCL obs broadcast" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "mfma",
+                "achieved": achieved,
+                "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP64_PEAK_TFLOPS,
+                "traffic": traffic,
+                "kernel": f"solve_kernel<{abi.MAX_MEMBERS if k > 56 else ((k + 7) // 8) * 8},false>",
+                "note": "FP64 flops F(k,p) of SURVEY.md 8(d) per solve launch / HIP-event launch time (rank 0)",
+            },
+            "detail": {
+                "solved_per_step": solved / args.steps,
+                "ms_solve_per_step": ms_solve / args.steps,
+                "ms_search_per_step": ms_search / args.steps,
+                "ms_prep_per_step": sum(s.ms_prep for s in stats) / args.steps,
+                "max_sweeps": max(s.max_sweeps for s in stats),
+                "nonconverged": sum(s.nonconverged for s in stats),
+                "obs_bcast_ms": bcast_ms,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(w)
+        print(json.dumps(out), flush=True)
+    core.finalize()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,637 @@
+// cwbl_abi.hip — C ABI of the LETKF analysis core (include/cwb_letkf_core.h).
+//
+// Host orchestration of one variable, mirroring letkf_driver (module_letkf_core.f90:59-297):
+//   build_tree x2        -> host kdtree2-compatible build, upload (kdtree_build.cpp)
+//   (point-independent)  -> obs_prep_kernel per obs type (QC / mean / spread columns)
+//   points :209-240      -> batches of {search_kernel, solve_kernel<KP>} on one HIP stream
+// The library owns its device buffers between cwbl_set_obs and cwbl_finalize; host arrays
+// handed in are copied inside the call.  There is no CPU fallback: without a gfx950 device
+// every compute entry point fails with CWBL_ERR_NO_DEVICE.
+#include "../../include/cwb_letkf_core.h"
+#include "cwbl_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace cwbl {
+namespace {
+
+std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(CWBL_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),     \
+                  __FILE__, __LINE__);                                                     \
+  } while (0)
+
+// grow-only device buffer
+struct DevBuf {
+  void *p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+    if (e == hipSuccess) n = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+struct ObsType {
+  int family = 0, type_id = 0, nvar = 1, nobs = 0;
+  std::vector<float> xyz;   // host copy (3,nobs) for tree builds
+  DevBuf obs, error, hdxb, qc;
+};
+
+struct TreeBufs {
+  DevBuf nodes, rdata, ind, col_bg, col_omm, col_err, col_ok;
+  HostTree host;
+};
+
+struct State {
+  bool inited = false;
+  int k = 0, kp = 0, device = 0, wf = 0, q1_mode = 0;
+  float norain = -5.0f;
+  size_t ws_bytes = size_t(2) << 30;
+  hipStream_t stream = nullptr;
+  std::vector<ObsType> obs;  // gts entries first (family 0), then radar (family 1)
+  bool have_obs = false;
+  std::vector<std::unique_ptr<TreeBufs>> trees;
+  DevBuf tdesc, nbr_cnt, nbr_idx, nbr_r2, info, stats;
+  DevBuf sx, sy, salt, svar;                          // slab staging (host-memory calls)
+  DevBuf bcol, byo, byb, bxb, bxa, bev;               // solve_batch staging
+  DevBuf qxyz, qnf, qidx, qr2;                        // search staging
+  std::vector<hipEvent_t> events;
+};
+
+State S;
+
+float search_r2() {
+  const float gc1999 = 2.0f * std::sqrt(10.0f / 3.0f);  // module_param.f90:116
+  return gc1999 * gc1999;                               // module_localization.f90:202
+}
+
+bool is_gts_assimilated(int id) {  // module_localization.f90:59-72
+  return id == CWBL_GTS_SYNOP || id == CWBL_GTS_METAR || id == CWBL_GTS_SHIPS ||
+         id == CWBL_GTS_SOUND || id == CWBL_GTS_GPSPW;
+}
+
+int tree_depth(const HostTree &t, int node = 0) {
+  if (t.nodes.empty()) return 0;
+  int depth = 0;
+  // iterative DFS over (node, level)
+  std::vector<std::pair<int, int>> st{{node, 1}};
+  while (!st.empty()) {
+    auto [nd, lv] = st.back();
+    st.pop_back();
+    depth = std::max(depth, lv);
+    if (t.nodes[nd].cut_dim >= 0) {
+      st.push_back({t.nodes[nd].left, lv + 1});
+      st.push_back({t.nodes[nd].right, lv + 1});
+    }
+  }
+  return depth;
+}
+
+// copy an array given by the caller (host or device) into a library device buffer
+hipError_t stage(DevBuf &dst, const void *src, size_t bytes, int memory) {
+  hipError_t e = dst.ensure(bytes);
+  if (e != hipSuccess || bytes == 0) return e;
+  return hipMemcpyAsync(dst.p, src, bytes,
+                        memory == CWBL_MEM_DEVICE ? hipMemcpyDeviceToDevice
+                                                  : hipMemcpyHostToDevice,
+                        S.stream);
+}
+
+hipError_t event(int i, hipEvent_t *out) {
+  while ((int)S.events.size() <= i) {
+    hipEvent_t e;
+    hipError_t r = hipEventCreate(&e);
+    if (r != hipSuccess) return r;
+    S.events.push_back(e);
+  }
+  *out = S.events[i];
+  return hipSuccess;
+}
+
+float elapsed(int a, int b) {
+  float ms = 0.0f;
+  if (hipEventElapsedTime(&ms, S.events[a], S.events[b]) != hipSuccess) return 0.0f;
+  return ms;
+}
+
+int require_device() {
+  if (!S.inited) return fail(CWBL_ERR_STATE, "cwbl_init has not been called");
+  return CWBL_OK;
+}
+
+// Builds the trees of one family (build_tree, module_localization.f90:35-167) and their
+// column tables.  Appends TreeDesc entries.
+int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &descs,
+                 int &list_cap) {
+  struct Pending { int entry; int type_id; const cwbl_type_params *tp; float hinv, vinv; };
+  std::vector<Pending> pend;
+  const int ntypes = family == 0 ? CWBL_NUM_GTS_TYPES : CWBL_NUM_RADAR_TYPES;
+  for (int id = 1; id <= ntypes; ++id) {
+    int entry = -1;
+    for (size_t e = 0; e < S.obs.size(); ++e)
+      if (S.obs[e].family == family && S.obs[e].type_id == id) entry = (int)e;
+    if (entry < 0 || S.obs[entry].nobs <= 0) continue;
+    if (family == 0 && !is_gts_assimilated(id)) continue;
+    const cwbl_type_params *tp = family == 0 ? &vp->gts[id - 1] : &vp->radar[id - 1];
+    if (!(tp->use_it && tp->hclr > 0.0f)) continue;
+    if (tp->max_lz_pts < 0) return fail(CWBL_ERR_ARG, "max_lz_pts < 0 for type %d", id);
+    const float hinv = 1.0f / (tp->hclr * 1e3f);
+    const float vinv = tp->vclr > 0.0f ? 1.0f / (tp->vclr * 1e3f) : -1.0f;
+    pend.push_back({entry, id, tp, hinv, vinv});
+  }
+  if (pend.empty()) return CWBL_OK;
+  const bool fam3d = pend.back().vinv > 0.0f;  // Q1: the leftover vclr_inv (:151)
+  for (const Pending &pd : pend) {
+    ObsType &ot = S.obs[pd.entry];
+    const bool own3d = pd.vinv > 0.0f;
+    bool dim3 = S.q1_mode == CWBL_Q1_PER_TYPE ? own3d : fam3d;
+    int q1u = 0;
+    if (dim3 && !own3d) { dim3 = false; q1u = 1; }
+    const int n = ot.nobs;
+    std::vector<float> nx(3 * (size_t)n);
+    for (int j = 0; j < n; ++j) {
+      nx[3 * j + 0] = ot.xyz[3 * j + 0] * pd.hinv;
+      nx[3 * j + 1] = ot.xyz[3 * j + 1] * pd.hinv;
+      nx[3 * j + 2] = dim3 ? ot.xyz[3 * j + 2] * pd.vinv : -1.0f;
+    }
+    auto tb = std::make_unique<TreeBufs>();
+    build_kdtree(nx.data(), n, dim3 ? 3 : 2, tb->host);
+    if (tree_depth(tb->host) >= kSearchStackDepth)
+      return fail(CWBL_ERR_UNSUPPORTED, "k-d tree too deep (%d obs)", n);
+    const HostTree &h = tb->host;
+    const size_t ncol = (size_t)n * ot.nvar;
+    HIPCHK(tb->nodes.ensure(h.nodes.size() * sizeof(TreeNode)));
+    HIPCHK(tb->rdata.ensure(h.rdata.size() * sizeof(float)));
+    HIPCHK(tb->ind.ensure(h.ind.size() * sizeof(int) + 4));
+    HIPCHK(tb->col_bg.ensure(ncol * S.kp * sizeof(float)));
+    HIPCHK(tb->col_omm.ensure(ncol * sizeof(float)));
+    HIPCHK(tb->col_err.ensure(ncol * sizeof(float)));
+    HIPCHK(tb->col_ok.ensure(ncol));
+    HIPCHK(hipMemcpyAsync(tb->nodes.p, h.nodes.data(), h.nodes.size() * sizeof(TreeNode),
+                          hipMemcpyHostToDevice, S.stream));
+    HIPCHK(hipMemcpyAsync(tb->rdata.p, h.rdata.data(), h.rdata.size() * sizeof(float),
+                          hipMemcpyHostToDevice, S.stream));
+    if (!h.ind.empty())
+      HIPCHK(hipMemcpyAsync(tb->ind.p, h.ind.data(), h.ind.size() * sizeof(int),
+                            hipMemcpyHostToDevice, S.stream));
+    // point-independent QC columns (letkf_yoyb :429-437 / :497-510)
+    const cwbl_type_params *tp = pd.tp;
+    int is_assim[5] = {0, 0, 0, 0, 0};
+    if (family == 0) {
+      for (int v = 0; v < ot.nvar; ++v) is_assim[v] = tp->hclr > 0.0f ? tp->is_assim[v] : 0;
+    } else {
+      is_assim[0] = tp->hclr > 0.0f ? 1 : 0;
+    }
+    HIPCHK(launch_obs_prep(S.stream, S.k, S.kp, family, ot.type_id, ot.nvar, n,
+                           ot.obs.as<float>(), ot.error.as<float>(), ot.hdxb.as<float>(),
+                           ot.qc.as<int>(), tp->err_muti, tp->err_rej, is_assim, S.norain,
+                           tb->col_bg.as<float>(), tb->col_omm.as<float>(),
+                           tb->col_err.as<float>(), tb->col_ok.as<uint8_t>()));
+    TreeDesc d{};
+    d.nodes = tb->nodes.as<TreeNode>();
+    d.rdata = tb->rdata.as<float4>();
+    d.ind = tb->ind.as<int>();
+    d.col_bg = tb->col_bg.as<float>();
+    d.col_omm = tb->col_omm.as<float>();
+    d.col_err = tb->col_err.as<float>();
+    d.col_ok = tb->col_ok.as<uint8_t>();
+    d.hclr_inv = pd.hinv;
+    d.vclr_inv = pd.vinv;
+    d.tree_dim = dim3 ? 3 : 2;
+    d.query3d = own3d ? 1 : 0;
+    d.nvar = ot.nvar;
+    d.max_lz = tp->max_lz_pts;
+    d.list_off = list_cap;
+    d.q1_undef = q1u;
+    list_cap += tp->max_lz_pts;
+    descs.push_back(d);
+    S.trees.push_back(std::move(tb));
+  }
+  return CWBL_OK;
+}
+
+void release_obs() {
+  for (auto &o : S.obs) {
+    o.obs.release(); o.error.release(); o.hdxb.release(); o.qc.release();
+  }
+  S.obs.clear();
+  S.have_obs = false;
+}
+
+void release_all() {
+  release_obs();
+  for (auto &t : S.trees) {
+    t->nodes.release(); t->rdata.release(); t->ind.release(); t->col_bg.release();
+    t->col_omm.release(); t->col_err.release(); t->col_ok.release();
+  }
+  S.trees.clear();
+  for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.nbr_r2, &S.info, &S.stats, &S.sx,
+                    &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev,
+                    &S.qxyz, &S.qnf, &S.qidx, &S.qr2})
+    b->release();
+  for (hipEvent_t e : S.events) (void)hipEventDestroy(e);
+  S.events.clear();
+  if (S.stream) (void)hipStreamDestroy(S.stream);
+  S.stream = nullptr;
+  S.inited = false;
+}
+
+SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps, float rtps_a) {
+  SolveConsts c{};
+  c.k = S.k;
+  c.kp = S.kp;
+  c.weight_function = S.wf;
+  c.inflat = inflat;
+  c.use_rtpp = use_rtpp;
+  c.use_rtps = use_rtps;
+  c.rtpp_alpha = rtpp_a;
+  c.rtps_alpha = rtps_a;
+  c.nmember_inv = 1.0f / (float)S.k;
+  c.r2 = search_r2();
+  return c;
+}
+
+}  // namespace
+}  // namespace cwbl
+
+using namespace cwbl;
+
+extern "C" {
+
+int cwbl_abi_version(void) { return CWBL_ABI_VERSION; }
+
+const char *cwbl_last_error(void) { return g_err.c_str(); }
+
+int cwbl_init(const cwbl_init_params *p) {
+  if (!p) return fail(CWBL_ERR_ARG, "cwbl_init: null params");
+  if (S.inited) release_all();
+  if (p->nmember < 2) return fail(CWBL_ERR_ARG, "nmember must be >= 2 (got %d)", p->nmember);
+  const int kp = supported_kp(p->nmember);
+  if (kp < 0)
+    return fail(CWBL_ERR_UNSUPPORTED, "nmember %d > %d not supported by this build",
+                p->nmember, CWBL_MAX_MEMBERS);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(CWBL_ERR_NO_DEVICE, "no HIP device available (the core has no CPU path)");
+  int dev = p->device;
+  if (dev < 0) HIPCHK(hipGetDevice(&dev));
+  if (dev >= ndev) return fail(CWBL_ERR_NO_DEVICE, "device %d >= device count %d", dev, ndev);
+  HIPCHK(hipSetDevice(dev));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, dev));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(CWBL_ERR_NO_DEVICE, "device %d is %s; this library is built for gfx950", dev,
+                prop.gcnArchName);
+  if (p->weight_function != 0 && p->weight_function != 1)
+    return fail(CWBL_ERR_ARG, "weight_function must be 0 or 1");
+  S.k = p->nmember;
+  S.kp = kp;
+  S.device = dev;
+  S.wf = p->weight_function;
+  S.norain = p->norain_value;
+  S.q1_mode = p->q1_mode;
+  S.ws_bytes = p->workspace_bytes ? p->workspace_bytes : (size_t(2) << 30);
+  HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+  S.inited = true;
+  return CWBL_OK;
+}
+
+int cwbl_finalize(void) {
+  if (S.inited) {
+    (void)hipStreamSynchronize(S.stream);
+    release_all();
+  }
+  return CWBL_OK;
+}
+
+int cwbl_set_obs(const cwbl_obs_set *o) {
+  if (int rc = require_device()) return rc;
+  if (!o) return fail(CWBL_ERR_ARG, "null obs set");
+  if (o->n_gts < 0 || o->n_radar < 0 || (o->n_gts && !o->gts) || (o->n_radar && !o->radar))
+    return fail(CWBL_ERR_ARG, "bad obs set counts/pointers");
+  release_obs();
+  const int mem = o->memory;
+  const size_t k = (size_t)S.k;
+  bool seen_g[CWBL_NUM_GTS_TYPES + 1] = {}, seen_r[CWBL_NUM_RADAR_TYPES + 1] = {};
+  for (int e = 0; e < o->n_gts; ++e) {
+    const cwbl_gts_obs &g = o->gts[e];
+    if (g.type_id < 1 || g.type_id > CWBL_NUM_GTS_TYPES || seen_g[g.type_id])
+      return fail(CWBL_ERR_ARG, "gts entry %d: bad or duplicate type_id %d", e, g.type_id);
+    if (g.nvar < 1 || g.nvar > CWBL_MAX_NVAR || g.nobs < 0)
+      return fail(CWBL_ERR_ARG, "gts type %d: bad nvar/nobs", g.type_id);
+    if (g.nobs > 0 && (!g.xyz || !g.obs || !g.error || !g.hdxb || !g.qc))
+      return fail(CWBL_ERR_ARG, "gts type %d: null array", g.type_id);
+    seen_g[g.type_id] = true;
+    S.obs.emplace_back();
+    ObsType &t = S.obs.back();
+    t.family = 0; t.type_id = g.type_id; t.nvar = g.nvar; t.nobs = g.nobs;
+    const size_t n = (size_t)g.nobs, nv = (size_t)g.nvar;
+    t.xyz.resize(3 * n);
+    if (n) {
+      if (mem == CWBL_MEM_DEVICE)
+        HIPCHK(hipMemcpy(t.xyz.data(), g.xyz, 3 * n * 4, hipMemcpyDeviceToHost));
+      else
+        std::memcpy(t.xyz.data(), g.xyz, 3 * n * 4);
+    }
+    HIPCHK(stage(t.obs, g.obs, n * nv * 4, mem));
+    HIPCHK(stage(t.error, g.error, n * nv * 4, mem));
+    HIPCHK(stage(t.hdxb, g.hdxb, n * nv * k * 4, mem));
+    HIPCHK(stage(t.qc, g.qc, n * nv * k * 4, mem));
+  }
+  for (int e = 0; e < o->n_radar; ++e) {
+    const cwbl_radar_obs &r = o->radar[e];
+    if (r.type_id < 1 || r.type_id > CWBL_NUM_RADAR_TYPES || seen_r[r.type_id])
+      return fail(CWBL_ERR_ARG, "radar entry %d: bad or duplicate type_id %d", e, r.type_id);
+    if (r.nobs < 0) return fail(CWBL_ERR_ARG, "radar type %d: bad nobs", r.type_id);
+    if (r.nobs > 0 && (!r.xyz || !r.obs || !r.hdxb))
+      return fail(CWBL_ERR_ARG, "radar type %d: null array", r.type_id);
+    seen_r[r.type_id] = true;
+    S.obs.emplace_back();
+    ObsType &t = S.obs.back();
+    t.family = 1; t.type_id = r.type_id; t.nvar = 1; t.nobs = r.nobs;
+    const size_t n = (size_t)r.nobs;
+    t.xyz.resize(3 * n);
+    if (n) {
+      if (mem == CWBL_MEM_DEVICE)
+        HIPCHK(hipMemcpy(t.xyz.data(), r.xyz, 3 * n * 4, hipMemcpyDeviceToHost));
+      else
+        std::memcpy(t.xyz.data(), r.xyz, 3 * n * 4);
+    }
+    HIPCHK(stage(t.obs, r.obs, n * 4, mem));
+    HIPCHK(stage(t.hdxb, r.hdxb, n * k * 4, mem));
+  }
+  HIPCHK(hipStreamSynchronize(S.stream));
+  S.have_obs = true;
+  return CWBL_OK;
+}
+
+int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats *stats) {
+  if (int rc = require_device()) return rc;
+  if (!S.have_obs) return fail(CWBL_ERR_STATE, "cwbl_set_obs has not been called");
+  if (!vp || !sl) return fail(CWBL_ERR_ARG, "null argument");
+  if (sl->nx < 0 || sl->ny < 0 || sl->nz < 0 || sl->ix_lim < 0 || sl->iy_lim < 0 ||
+      sl->ix_lim > sl->nx || sl->iy_lim > sl->ny || sl->ix_lim > sl->alt_nx ||
+      sl->iy_lim > sl->alt_ny)
+    return fail(CWBL_ERR_ARG, "slab bounds: nx=%d ny=%d ix_lim=%d iy_lim=%d alt=%dx%d",
+                sl->nx, sl->ny, sl->ix_lim, sl->iy_lim, sl->alt_nx, sl->alt_ny);
+  if (!(vp->multi_infl > 0.0f)) return fail(CWBL_ERR_ARG, "multi_infl must be > 0");
+  const auto t_start = std::chrono::steady_clock::now();
+  cwbl_stats st;
+  std::memset(&st, 0, sizeof st);
+  const long long npts = (long long)sl->ix_lim * sl->iy_lim * sl->nz;
+  st.points = npts;
+
+  hipEvent_t e0, e1;
+  HIPCHK(event(0, &e0));
+  HIPCHK(hipEventRecord(e0, S.stream));
+  // ---- trees + column tables ------------------------------------------------------------
+  for (auto &t : S.trees) {
+    t->nodes.release(); t->rdata.release(); t->ind.release(); t->col_bg.release();
+    t->col_omm.release(); t->col_err.release(); t->col_ok.release();
+  }
+  S.trees.clear();
+  std::vector<TreeDesc> descs;
+  int list_cap = 0;
+  if (int rc = build_family(0, vp, descs, list_cap)) return rc;
+  if (int rc = build_family(1, vp, descs, list_cap)) return rc;
+  const int nt = (int)descs.size();
+  st.ntrees = nt;
+  if (nt == 0 || npts == 0) {  // `if(all(.not. succeed)) cycle` (:66)
+    HIPCHK(hipStreamSynchronize(S.stream));
+    st.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    if (stats) *stats = st;
+    return CWBL_OK;
+  }
+  for (const TreeDesc &d : descs) st.q1_undefined += d.q1_undef ? npts : 0;
+  HIPCHK(S.tdesc.ensure(descs.size() * sizeof(TreeDesc)));
+  HIPCHK(hipMemcpyAsync(S.tdesc.p, descs.data(), descs.size() * sizeof(TreeDesc),
+                        hipMemcpyHostToDevice, S.stream));
+  HIPCHK(event(1, &e1));
+  HIPCHK(hipEventRecord(e1, S.stream));
+
+  // ---- slab ---------------------------------------------------------------------------------
+  const long long L = (long long)sl->nx * sl->ny * sl->nz;
+  SlabDev sd{};
+  sd.nx = sl->nx; sd.ny = sl->ny; sd.nz = sl->nz; sd.alt_nx = sl->alt_nx;
+  sd.alt_ny = sl->alt_ny; sd.ix_lim = sl->ix_lim; sd.iy_lim = sl->iy_lim; sd.L = L;
+  const size_t bxy = (size_t)sl->nx * sl->ny * 4;
+  const size_t balt = (size_t)sl->alt_nx * sl->alt_ny * sl->nz * 4;
+  const size_t bvar = (size_t)L * S.k * 4;
+  hipEvent_t e2;
+  HIPCHK(event(2, &e2));
+  if (sl->memory == CWBL_MEM_DEVICE) {
+    sd.x = sl->x; sd.y = sl->y; sd.alt = sl->alt; sd.var = sl->var;
+  } else {
+    HIPCHK(stage(S.sx, sl->x, bxy, CWBL_MEM_HOST));
+    HIPCHK(stage(S.sy, sl->y, bxy, CWBL_MEM_HOST));
+    HIPCHK(stage(S.salt, sl->alt, balt, CWBL_MEM_HOST));
+    HIPCHK(stage(S.svar, sl->var, bvar, CWBL_MEM_HOST));
+    sd.x = S.sx.as<float>(); sd.y = S.sy.as<float>(); sd.alt = S.salt.as<float>();
+    sd.var = S.svar.as<float>();
+  }
+  HIPCHK(hipEventRecord(e2, S.stream));
+
+  // ---- batches of {search, solve} ---------------------------------------------------------
+  const size_t per_pt = (size_t)list_cap * 8 + (size_t)nt * 4 + 8;
+  long long B = (long long)(S.ws_bytes / per_pt);
+  B = std::max<long long>(std::min<long long>(B, npts), 256);
+  B = std::min<long long>(B, 1 << 22);
+  HIPCHK(S.nbr_cnt.ensure((size_t)B * nt * 4));
+  HIPCHK(S.nbr_idx.ensure((size_t)B * std::max(list_cap, 1) * 4));
+  HIPCHK(S.nbr_r2.ensure((size_t)B * std::max(list_cap, 1) * 4));
+  HIPCHK(S.info.ensure((size_t)B * sizeof(int2)));
+  HIPCHK(S.stats.ensure(sizeof(DevStats)));
+  HIPCHK(hipMemsetAsync(S.stats.p, 0, sizeof(DevStats), S.stream));
+  SolveConsts c = solve_consts((float)(S.k - 1) / vp->multi_infl,  // inflat (:68)
+                               vp->use_rtpp, vp->rtpp_alpha, vp->use_rtps, vp->rtps_alpha);
+  c.ntrees = nt;
+  c.list_cap = list_cap;
+  const TreeDesc *dtrees = S.tdesc.as<TreeDesc>();
+  DevStats *dst = S.stats.as<DevStats>();
+  int ev = 3;
+  std::vector<std::pair<int, int>> search_ev, solve_ev;
+  for (long long g0 = 0; g0 < npts; g0 += B) {
+    const int nb = (int)std::min<long long>(B, npts - g0);
+    hipEvent_t a, b, cc;
+    HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b)); HIPCHK(event(ev + 2, &cc));
+    HIPCHK(hipEventRecord(a, S.stream));
+    HIPCHK(launch_search(S.stream, dtrees, nt, list_cap, c.r2, sd, g0, nb,
+                         S.nbr_cnt.as<int>(), S.nbr_idx.as<int>(), S.nbr_r2.as<float>(), dst));
+    HIPCHK(hipEventRecord(b, S.stream));
+    HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, S.nbr_cnt.as<int>(),
+                                  S.nbr_idx.as<int>(), S.nbr_r2.as<float>(),
+                                  S.info.as<int2>()));
+    HIPCHK(hipEventRecord(cc, S.stream));
+    HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), nb, dst));
+    search_ev.push_back({ev, ev + 1});
+    solve_ev.push_back({ev + 1, ev + 2});
+    ev += 3;
+  }
+  hipEvent_t e_end;
+  HIPCHK(event(ev, &e_end));
+  if (sl->memory != CWBL_MEM_DEVICE)
+    HIPCHK(hipMemcpyAsync(sl->var, S.svar.p, bvar, hipMemcpyDeviceToHost, S.stream));
+  HIPCHK(hipEventRecord(e_end, S.stream));
+  DevStats ds;
+  HIPCHK(hipMemcpyAsync(&ds, S.stats.p, sizeof ds, hipMemcpyDeviceToHost, S.stream));
+  HIPCHK(hipStreamSynchronize(S.stream));
+
+  st.solved = (long long)ds.solved;
+  st.nobs_sum = (long long)ds.nobs_sum;
+  st.lz_truncated = (long long)ds.lz_truncated;
+  st.nonconverged = (long long)ds.nonconverged;
+  st.max_p = (int)ds.max_p;
+  st.max_sweeps = (int)ds.max_sweeps;
+  st.ms_prep = elapsed(0, 1);
+  for (auto &p : search_ev) st.ms_search += elapsed(p.first, p.second);
+  for (auto &p : solve_ev) st.ms_solve += elapsed(p.first, p.second);
+  st.ms_copy = elapsed(1, 2) + (sl->memory != CWBL_MEM_DEVICE ? elapsed(ev - 1, ev) : 0.0f);
+  st.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  if (stats) *stats = st;
+  return CWBL_OK;
+}
+
+int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const float *yb,
+                     const float *xb, float inflat, int use_rtpp, float rtpp_alpha,
+                     int use_rtps, float rtps_alpha, float *xa, double *evals, int memory) {
+  if (int rc = require_device()) return rc;
+  if (npts < 0 || (npts > 0 && (!col_off || !xb || !xa)))
+    return fail(CWBL_ERR_ARG, "cwbl_solve_batch: bad arguments");
+  if (npts == 0) return CWBL_OK;
+  const size_t k = (size_t)S.k;
+  std::vector<long long> hoff;
+  const long long *doff = col_off;
+  long long ncol;
+  if (memory == CWBL_MEM_DEVICE) {
+    HIPCHK(hipMemcpy(&ncol, col_off + npts, 8, hipMemcpyDeviceToHost));
+  } else {
+    ncol = col_off[npts];
+    for (int i = 0; i < npts; ++i)
+      if (col_off[i + 1] < col_off[i]) return fail(CWBL_ERR_ARG, "col_off not monotone");
+  }
+  if (ncol > 0 && (!yo || !yb)) return fail(CWBL_ERR_ARG, "cwbl_solve_batch: null yo/yb");
+  const float *dyo = yo, *dyb = yb, *dxb = xb;
+  float *dxa = xa;
+  double *dev = evals;
+  if (memory != CWBL_MEM_DEVICE) {
+    HIPCHK(stage(S.bcol, col_off, (size_t)(npts + 1) * 8, memory));
+    HIPCHK(stage(S.byo, yo, (size_t)ncol * 4, memory));
+    HIPCHK(stage(S.byb, yb, (size_t)ncol * k * 4, memory));
+    HIPCHK(stage(S.bxb, xb, (size_t)npts * k * 4, memory));
+    HIPCHK(S.bxa.ensure((size_t)npts * k * 4));
+    if (evals) HIPCHK(S.bev.ensure((size_t)npts * k * 8));
+    doff = S.bcol.as<long long>(); dyo = S.byo.as<float>(); dyb = S.byb.as<float>();
+    dxb = S.bxb.as<float>(); dxa = S.bxa.as<float>(); dev = evals ? S.bev.as<double>() : nullptr;
+  }
+  HIPCHK(S.info.ensure((size_t)npts * sizeof(int2)));
+  SolveConsts c = solve_consts(inflat, use_rtpp, rtpp_alpha, use_rtps, rtps_alpha);
+  HIPCHK(launch_solve_assembled(S.stream, S.kp, c, npts, doff, dyo, dyb, dxb, dxa, dev,
+                                S.info.as<int2>()));
+  if (memory != CWBL_MEM_DEVICE) {
+    HIPCHK(hipMemcpyAsync(xa, dxa, (size_t)npts * k * 4, hipMemcpyDeviceToHost, S.stream));
+    if (evals)
+      HIPCHK(hipMemcpyAsync(evals, dev, (size_t)npts * k * 8, hipMemcpyDeviceToHost, S.stream));
+  }
+  HIPCHK(hipStreamSynchronize(S.stream));
+  return CWBL_OK;
+}
+
+int cwbl_search(int nobs, const float *obs_xyz, float hclr, float vclr, int max_lz_pts,
+                int nq, const float *q_xyz, int *nfound, int *idx, float *r2, int memory) {
+  if (int rc = require_device()) return rc;
+  if (nobs < 0 || nq < 0 || max_lz_pts < 1 || !(hclr > 0.0f))
+    return fail(CWBL_ERR_ARG, "cwbl_search: bad arguments");
+  if (memory == CWBL_MEM_DEVICE)
+    return fail(CWBL_ERR_UNSUPPORTED, "cwbl_search takes host arrays");
+  const float hinv = 1.0f / (hclr * 1e3f);
+  const float vinv = vclr > 0.0f ? 1.0f / (vclr * 1e3f) : -1.0f;
+  const bool dim3 = vinv > 0.0f;
+  std::vector<float> nx(3 * (size_t)nobs);
+  for (int j = 0; j < nobs; ++j) {
+    nx[3 * j] = obs_xyz[3 * j] * hinv;
+    nx[3 * j + 1] = obs_xyz[3 * j + 1] * hinv;
+    nx[3 * j + 2] = dim3 ? obs_xyz[3 * j + 2] * vinv : -1.0f;
+  }
+  TreeBufs tb;
+  build_kdtree(nx.data(), nobs, dim3 ? 3 : 2, tb.host);
+  if (tree_depth(tb.host) >= kSearchStackDepth)
+    return fail(CWBL_ERR_UNSUPPORTED, "k-d tree too deep");
+  const HostTree &h = tb.host;
+  HIPCHK(tb.nodes.ensure(std::max<size_t>(h.nodes.size(), 1) * sizeof(TreeNode)));
+  HIPCHK(tb.rdata.ensure(h.rdata.size() * sizeof(float)));
+  HIPCHK(tb.ind.ensure(h.ind.size() * sizeof(int) + 4));
+  if (!h.nodes.empty())
+    HIPCHK(hipMemcpyAsync(tb.nodes.p, h.nodes.data(), h.nodes.size() * sizeof(TreeNode),
+                          hipMemcpyHostToDevice, S.stream));
+  HIPCHK(hipMemcpyAsync(tb.rdata.p, h.rdata.data(), h.rdata.size() * sizeof(float),
+                        hipMemcpyHostToDevice, S.stream));
+  if (nobs)
+    HIPCHK(hipMemcpyAsync(tb.ind.p, h.ind.data(), h.ind.size() * sizeof(int),
+                          hipMemcpyHostToDevice, S.stream));
+  TreeDesc d{};
+  d.nodes = tb.nodes.as<TreeNode>();
+  d.rdata = tb.rdata.as<float4>();
+  d.ind = tb.ind.as<int>();
+  d.hclr_inv = hinv;
+  d.vclr_inv = vinv;
+  d.tree_dim = dim3 ? 3 : 2;
+  d.query3d = dim3 ? 1 : 0;
+  d.nvar = 1;
+  d.max_lz = nobs > 0 ? max_lz_pts : 0;
+  d.list_off = 0;
+  DevBuf dd;
+  HIPCHK(dd.ensure(sizeof d));
+  HIPCHK(hipMemcpyAsync(dd.p, &d, sizeof d, hipMemcpyHostToDevice, S.stream));
+  HIPCHK(stage(S.qxyz, q_xyz, (size_t)nq * 12, CWBL_MEM_HOST));
+  HIPCHK(S.qnf.ensure((size_t)nq * 4));
+  HIPCHK(S.qidx.ensure((size_t)nq * max_lz_pts * 4));
+  HIPCHK(S.qr2.ensure((size_t)nq * max_lz_pts * 4));
+  HIPCHK(launch_search_single(S.stream, dd.as<TreeDesc>(), search_r2(), nq, S.qxyz.as<float>(),
+                              max_lz_pts, S.qnf.as<int>(), S.qidx.as<int>(), S.qr2.as<float>()));
+  HIPCHK(hipMemcpyAsync(nfound, S.qnf.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S.stream));
+  HIPCHK(hipMemcpyAsync(idx, S.qidx.p, (size_t)nq * max_lz_pts * 4, hipMemcpyDeviceToHost,
+                        S.stream));
+  HIPCHK(hipMemcpyAsync(r2, S.qr2.p, (size_t)nq * max_lz_pts * 4, hipMemcpyDeviceToHost,
+                        S.stream));
+  HIPCHK(hipStreamSynchronize(S.stream));
+  dd.release();
+  tb.nodes.release(); tb.rdata.release(); tb.ind.release();
+  return CWBL_OK;
+}
+
+}  // extern "C"

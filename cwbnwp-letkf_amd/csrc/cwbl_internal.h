@@ -1,0 +1,114 @@
+// cwbl_internal.h — data layouts shared by the host orchestration (cwbl_abi.hip),
+// the host k-d tree builder (kdtree_build.cpp) and the HIP kernels (cwbl_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+namespace cwbl {
+
+// One node of a flattened kdtree2 tree (module_kdtree2.f90:512-528).  64 bytes.
+struct TreeNode {
+  float cut_val, cut_val_left, cut_val_right;
+  int   cut_dim;          // 0..2 for internal nodes, -1 for terminal (bucket) nodes
+  float lo[3];            // node%box(:)%lower (final, union of children)
+  float hi[3];            // node%box(:)%upper
+  int   left, right;      // child node indices (-1 = null)
+  int   l, u;             // inclusive range into the permuted data
+  int   pad_[2];
+};
+static_assert(sizeof(TreeNode) == 64, "TreeNode layout");
+
+// Host-side result of building one tree.
+struct HostTree {
+  int dim = 3;
+  int n = 0;
+  std::vector<TreeNode> nodes;     // root = 0
+  std::vector<int>      ind;       // permutation (0-based obs index of rearranged slot)
+  std::vector<float>    rdata;     // rearranged normalised coords, 4 floats per slot
+};
+
+// kdtree2_create(xyz(3,n), dim) with the reference's settings (bucket 12, exact median,
+// rearranged data).  xyz3 is already normalised by hclr/vclr as in build_tree.
+void build_kdtree(const float *xyz3, int n, int dim, HostTree &out);
+
+// Per-tree descriptor handed to the kernels (device-resident array of these).
+struct TreeDesc {
+  const TreeNode *nodes;
+  const float4   *rdata;      // rearranged normalised coords (x,y,z,0)
+  const int      *ind;
+  // column table of this type for the current variable (one column per (obs, obs-var))
+  const float    *col_bg;     // [n*nvar][KP] fp32 bg = hdxb - mean, zero padded
+  const float    *col_omm;    // [n*nvar] obs - mean
+  const float    *col_err;    // [n*nvar] error * err_muti
+  const uint8_t  *col_ok;     // [n*nvar] accepted (is_assim, qc, gross-error tests)
+  float hclr_inv, vclr_inv;   // this type's own normalisation (get_lz)
+  int   tree_dim;             // dimension the tree was built with
+  int   query3d;              // this type queries in 3-D (own vclr > 0)
+  int   nvar;
+  int   max_lz;
+  int   list_off;             // offset of this type inside a point's neighbour list
+  int   q1_undef;
+};
+
+// Per-variable constants of the solve.
+struct SolveConsts {
+  int   k;
+  int   kp;                   // padded member count of the kernel instantiation
+  int   ntrees;
+  int   list_cap;             // sum of max_lz over trees
+  int   weight_function;
+  int   use_rtpp, use_rtps;
+  float inflat, rtpp_alpha, rtps_alpha;
+  float nmember_inv;          // 1.0/k (module_param.f90:245)
+  float r2;                   // gc1999**2
+};
+
+// Point enumeration of a slab: g = i + ix_lim*(j + iy_lim*kz).
+struct SlabDev {
+  int nx, ny, nz, alt_nx, alt_ny, ix_lim, iy_lim;
+  long long L;                // nx*ny*nz (member stride of var)
+  const float *x, *y, *alt;
+  float *var;
+};
+
+// Device-side counters (atomics) reported through cwbl_stats.
+struct DevStats {
+  unsigned long long solved, nobs_sum, lz_truncated, nonconverged, q1_undefined;
+  unsigned int max_p, max_sweeps;
+};
+
+// Kernel launchers (cwbl_kernels.hip).
+hipError_t launch_obs_prep(hipStream_t s, int k, int kp, int family, int type_id, int nvar,
+                           int nobs, const float *obs, const float *error, const float *hdxb,
+                           const int *qc, const float err_muti[5], const float err_rej[5],
+                           const int is_assim[5], float norain, float *col_bg,
+                           float *col_omm, float *col_err, uint8_t *col_ok);
+
+hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int list_cap,
+                         float r2, SlabDev slab, long long g0, int npts, int *nbr_cnt,
+                         int *nbr_idx, float *nbr_r2, DevStats *stats);
+
+hipError_t launch_solve_neighbors(hipStream_t s, int kp, const TreeDesc *trees,
+                                  SolveConsts c, SlabDev slab, long long g0, int npts,
+                                  const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                                  int2 *info);
+
+hipError_t launch_solve_assembled(hipStream_t s, int kp, SolveConsts c, int npts,
+                                  const long long *col_off, const float *yo, const float *yb,
+                                  const float *xb, float *xa, double *evals, int2 *info);
+
+hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, float r2, int nq,
+                                const float *q_xyz, int max_lz, int *nfound, int *idx,
+                                float *r2out);
+
+hipError_t launch_reduce_info(hipStream_t s, const int2 *info, int n, DevStats *stats);
+
+constexpr int kSearchStackDepth = 40;  // max k-d tree depth the search kernel supports
+
+int supported_kp(int k);      // smallest compiled KP >= k, or -1
+
+}  // namespace cwbl

@@ -1,0 +1,833 @@
+// cwbl_kernels.hip — gfx950 kernels of the LETKF analysis core.
+//
+//   obs_prep_kernel   per (observation, obs-variable): the point-independent half of
+//                     letkf_yoyb (module_letkf_core.f90:429-437, 497-510): ensemble mean,
+//                     perturbations, spread, error, QC and gross-error decision -> column table
+//   search_kernel     one lane per grid point: get_lz -> kdtree2_r_nearest for every tree
+//                     (module_localization.f90:188-331, module_kdtree2.f90:1118-1712), same
+//                     neighbours in the same traversal order, truncated at max_lz_pts
+//   solve_kernel<KP>  one wavefront per grid point: the point-dependent half of letkf_yoyb
+//                     (localisation weight, :443-452) + letkf_solve (:598-700): fp64
+//                     Yb Yb^T accumulation, parallel cyclic Jacobi eigensolver with A in LDS
+//                     and the eigenvector rows in VGPRs, W^a / wbar^a applied matrix-free,
+//                     RTPP/RTPS epilogue in the reference's fp32 operation order.
+//
+// Built with -ffp-contract=off: every fp32 expression is evaluated unfused, in the
+// reference's order (amdflang x86-64 evaluates the Fortran that way; see oracle/).
+// fp64 code uses explicit fma() where a fused result is wanted.
+#include "cwbl_internal.h"
+
+#include <hip/hip_runtime.h>
+
+namespace cwbl {
+
+// ---------------------------------------------------------------------------------------
+// fp32 helpers that must round exactly like the reference build
+// ---------------------------------------------------------------------------------------
+__constant__ unsigned long long kExpT[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+
+// exp(real(4)) as the reference build evaluates it: glibc 2.35 expf, FMA variant
+// (table-driven, computed in double; the reference's flang `exp` calls libm expf).
+__device__ __forceinline__ float expf_ref(float x) {
+  const unsigned ux = __float_as_uint(x);
+  const unsigned abstop = (ux >> 20) & 0x7ffu;
+  if (abstop >= 0x42bu) {  // |x| >= 88: not reached on this path (0.25*r2 <= 3.34)
+    if (ux == 0xff800000u) return 0.0f;
+    return expf(x);
+  }
+  const double shift = __longlong_as_double(0x4338000000000000ll);
+  const double invln2n = __longlong_as_double(0x40471547652b82fell);
+  const double c0 = __longlong_as_double(0x3ebc6af84b912394ll);
+  const double c1 = __longlong_as_double(0x3f2ebfce50fac4f3ll);
+  const double c2 = __longlong_as_double(0x3f962e42ff0c52d6ll);
+  const double xd = (double)x;
+  double kd = fma(invln2n, xd, shift);
+  const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
+  kd = kd - shift;
+  const double r = fma(invln2n, xd, -kd);
+  unsigned long long t = kExpT[ki & 31ull];
+  t += ki << 47;
+  const double s = __longlong_as_double((long long)t);
+  const double z = fma(r, c0, c1);
+  const double r2 = r * r;
+  double y = fma(r, c2, 1.0);
+  y = fma(z, r2, y);
+  y = y * s;
+  return (float)y;
+}
+
+// Gaspari_Cohn_1999, module_localization.f90:333-364 (fp32, unfused)
+__device__ __forceinline__ float gaspari_cohn(float x) {
+  const float a = 1.82574189f;  // sqrt(10./3.) in fp32 (== sqrtf(10.0f/3.0f))
+  const float a1 = -0.25f, a2 = 0.5f, a3 = 0.625f, a4 = -5.0f / 3.0f, a5 = 1.0f;
+  const float b1 = 1.0f / 12.0f, b2 = -0.5f, b3 = 0.625f, b4 = 5.0f / 3.0f, b5 = -5.0f,
+              b6 = 4.0f, b7 = -2.0f / 3.0f;
+  const float z = x / a;
+  if (z <= 1.0f) return z * z * (z * (z * (a1 * z + a2) + a3) + a4) + a5;
+  if (z <= 2.0f) return z * (z * (z * (z * (b1 * z + b2) + b3) + b4) + b5) + b6 + b7 / z;
+  return 0.0f;
+}
+
+// localisation weight on the error, module_letkf_core.f90:443-450 / 516-523
+__device__ __forceinline__ float error_inv(int wf, float err, float r2) {
+  if (wf != 1) return 1.0f / (err * expf_ref(0.25f * r2));
+  return sqrtf(gaspari_cohn(sqrtf(r2))) / err;
+}
+
+// ---------------------------------------------------------------------------------------
+// obs_prep_kernel: one thread per column c = n*nvar + v of one obs type
+// ---------------------------------------------------------------------------------------
+struct PrepParams {
+  float err_muti[5], err_rej[5];
+  int is_assim[5];
+};
+
+__global__ void __launch_bounds__(256)
+obs_prep_kernel(int k, int kp, int family, int type_id, int nvar, int nobs,
+                const float *__restrict__ obs, const float *__restrict__ error,
+                const float *__restrict__ hdxb, const int *__restrict__ qc, PrepParams pp,
+                float norain, float *__restrict__ col_bg, float *__restrict__ col_omm,
+                float *__restrict__ col_err, uint8_t *__restrict__ col_ok) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long ncol = (long long)nobs * nvar;
+  if (c >= ncol) return;
+  const int n = (int)(c / nvar), v = (int)(c - (long long)n * nvar);
+  const long long mstride = ncol;  // hdxb(nvar,nobs,0:k-1): member stride = nvar*nobs
+  float *bg = col_bg + c * kp;
+  bool ok;
+  float omm = 0.0f, err = 0.0f;
+  if (family == 0) {
+    ok = pp.is_assim[v] != 0;
+    if (ok) {  // any(qc(k,idx,:) >= 0)   (:429)
+      bool anyqc = false;
+      for (int m = 0; m < k; ++m) anyqc |= qc[c + mstride * m] >= 0;
+      ok = anyqc;
+    }
+  } else {
+    ok = pp.is_assim[0] != 0;  // radar: hclr(ivar) > 0 (:487)
+  }
+  if (ok) {
+    const float ninv = 1.0f / (float)k, n1inv = 1.0f / (float)(k - 1);
+    float s = 0.0f;
+    for (int m = 0; m < k; ++m) s = s + hdxb[c + mstride * m];          // sum(bg)
+    const float mean = s * ninv;
+    float d = 0.0f;
+    for (int m = 0; m < k; ++m) {
+      const float b = hdxb[c + mstride * m] - mean;
+      bg[m] = b;
+      d = d + b * b;                                                    // dot_product(bg,bg)
+    }
+    const float o = obs[c];
+    omm = o - mean;
+    const float std = sqrtf(d * n1inv);
+    const float e = family == 0 ? error[c] * pp.err_muti[v] : pp.err_muti[0];
+    const float rej = family == 0 ? pp.err_rej[v] : pp.err_rej[0];
+    const bool gross = fabsf(omm) > sqrtf(std * std + e * e) * rej;
+    if (family == 1 && type_id == 1) {  // dbz, :504-507
+      if (gross && o != norain) ok = false;
+      if (o == norain && mean == norain) ok = false;
+    } else if (gross) {
+      ok = false;
+    }
+    err = e;
+  }
+  for (int m = ok ? k : 0; m < kp; ++m) bg[m] = 0.0f;
+  col_omm[c] = omm;
+  col_err[c] = err;
+  col_ok[c] = ok ? 1 : 0;
+}
+
+hipError_t launch_obs_prep(hipStream_t s, int k, int kp, int family, int type_id, int nvar,
+                           int nobs, const float *obs, const float *error, const float *hdxb,
+                           const int *qc, const float err_muti[5], const float err_rej[5],
+                           const int is_assim[5], float norain, float *col_bg,
+                           float *col_omm, float *col_err, uint8_t *col_ok) {
+  PrepParams pp;
+  for (int i = 0; i < 5; ++i) {
+    pp.err_muti[i] = err_muti[i];
+    pp.err_rej[i] = err_rej[i];
+    pp.is_assim[i] = is_assim[i];
+  }
+  const long long ncol = (long long)nobs * nvar;
+  if (ncol == 0) return hipSuccess;
+  const unsigned grid = (unsigned)((ncol + 255) / 256);
+  hipLaunchKernelGGL(obs_prep_kernel, dim3(grid), dim3(256), 0, s, k, kp, family, type_id,
+                     nvar, nobs, obs, error, hdxb, qc, pp, norain, col_bg, col_omm, col_err,
+                     col_ok);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// search_kernel: one lane per query point
+// ---------------------------------------------------------------------------------------
+constexpr int kStackDepth = kSearchStackDepth;
+
+__device__ __forceinline__ float dis2_from_bnd(float x, float amin, float amax) {
+  if (x > amax) return (x - amax) * (x - amax);
+  if (x < amin) return (amin - x) * (amin - x);
+  return 0.0f;
+}
+
+// kdtree2_r_nearest on one tree (fixed ball).  The recursion of search() (:1381-1457) is run
+// with an explicit stack: because the ball never shrinks in the fixed-ball search, the
+// decision to visit the farther child can be taken before descending the closer one, and
+// LIFO order then reproduces the recursive visiting order exactly.
+__device__ int search_tree(const TreeDesc &T, float q0, float q1, float q2, float r2,
+                           int *out_idx, float *out_r2, int *stk, bool &overflow) {
+  const TreeNode *__restrict__ nodes = T.nodes;
+  const int dim = T.tree_dim;
+  int count = 0, sp = 0, node = 0;
+  overflow = false;
+  while (true) {
+    const TreeNode nd = nodes[node];
+    if (nd.cut_dim < 0) {  // process_terminal_node_fixedball (:1654-1707)
+      for (int i = nd.l; i <= nd.u; ++i) {
+        const float4 d = T.rdata[i];
+        const float dx = d.x - q0, dy = d.y - q1;
+        float sd = dx * dx;
+        sd = sd + dy * dy;
+        if (dim == 3) {
+          const float dz = d.z - q2;
+          sd = sd + dz * dz;
+        }
+        if (sd <= r2) {
+          if (count == T.max_lz) { overflow = true; return count; }
+          out_idx[count] = T.ind[i];
+          out_r2[count] = sd;
+          ++count;
+        }
+      }
+      if (sp == 0) return count;
+      node = stk[--sp * 64];
+      continue;
+    }
+    const int cd = nd.cut_dim;
+    const float qval = cd == 0 ? q0 : (cd == 1 ? q1 : q2);
+    int closer, farther;
+    float dis;
+    if (qval < nd.cut_val) {
+      closer = nd.left; farther = nd.right;
+      dis = (nd.cut_val_right - qval) * (nd.cut_val_right - qval);
+    } else {
+      closer = nd.right; farther = nd.left;
+      dis = (nd.cut_val_left - qval) * (nd.cut_val_left - qval);
+    }
+    bool far_ok = farther >= 0 && dis <= r2;
+    if (far_ok) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        if (i >= dim || i == cd || !far_ok) continue;
+        const float qi = i == 0 ? q0 : (i == 1 ? q1 : q2);
+        dis = dis + dis2_from_bnd(qi, nd.lo[i], nd.hi[i]);
+        if (dis > r2) far_ok = false;
+      }
+    }
+    if (far_ok) stk[sp++ * 64] = farther;
+    node = closer;
+  }
+}
+
+struct SlabQuery {
+  SlabDev s;
+  long long g0;
+  __device__ void at(int gi, float &x, float &y, float &z) const {
+    const long long g = g0 + gi;
+    const int i = (int)(g % s.ix_lim);
+    const long long r = g / s.ix_lim;
+    const int j = (int)(r % s.iy_lim);
+    const int kz = (int)(r / s.iy_lim);
+    x = s.x[i + (long long)s.nx * j];
+    y = s.y[i + (long long)s.nx * j];
+    z = s.alt[i + (long long)s.alt_nx * (j + (long long)s.alt_ny * kz)];
+  }
+};
+
+struct ListQuery {
+  const float *q;  // (3,nq)
+  __device__ void at(int gi, float &x, float &y, float &z) const {
+    x = q[3 * (long long)gi];
+    y = q[3 * (long long)gi + 1];
+    z = q[3 * (long long)gi + 2];
+  }
+};
+
+template <class Q>
+__global__ void __launch_bounds__(64)
+search_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, float r2, Q qs,
+              int npts, int *__restrict__ nbr_cnt, int *__restrict__ nbr_idx,
+              float *__restrict__ nbr_r2, DevStats *stats) {
+  __shared__ int stk[kStackDepth * 64];
+  const int gi = blockIdx.x * 64 + threadIdx.x;
+  if (gi >= npts) return;
+  float px, py, pz;
+  qs.at(gi, px, py, pz);
+  unsigned trunc = 0;
+  for (int t = 0; t < ntrees; ++t) {
+    const TreeDesc &T = trees[t];
+    // get_lz normalisation (module_localization.f90:243-253)
+    const float q0 = px * T.hclr_inv, q1 = py * T.hclr_inv;
+    const float q2 = T.query3d ? pz * T.vclr_inv : 0.0f;
+    const long long base = (long long)gi * list_cap + T.list_off;
+    bool ovf = false;
+    int cnt = 0;
+    if (T.max_lz > 0)
+      cnt = search_tree(T, q0, q1, q2, r2, nbr_idx + base, nbr_r2 + base, stk + threadIdx.x,
+                        ovf);
+    nbr_cnt[(long long)gi * ntrees + t] = cnt;
+    trunc += ovf ? 1u : 0u;
+  }
+  if (trunc && stats) atomicAdd(&stats->lz_truncated, (unsigned long long)trunc);
+}
+
+hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int list_cap,
+                         float r2, SlabDev slab, long long g0, int npts, int *nbr_cnt,
+                         int *nbr_idx, float *nbr_r2, DevStats *stats) {
+  if (npts <= 0) return hipSuccess;
+  SlabQuery q{slab, g0};
+  hipLaunchKernelGGL(search_kernel<SlabQuery>, dim3((npts + 63) / 64), dim3(64), 0, s, trees,
+                     ntrees, list_cap, r2, q, npts, nbr_cnt, nbr_idx, nbr_r2, stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, float r2, int nq,
+                                const float *q_xyz, int max_lz, int *nfound, int *idx,
+                                float *r2out) {
+  if (nq <= 0) return hipSuccess;
+  ListQuery q{q_xyz};
+  hipLaunchKernelGGL(search_kernel<ListQuery>, dim3((nq + 63) / 64), dim3(64), 0, s, tree, 1,
+                     max_lz, r2, q, nq, nfound, idx, r2out, (DevStats *)nullptr);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// solve_kernel<KP>: one wavefront (64 lanes) per grid point, members padded to KP
+// ---------------------------------------------------------------------------------------
+constexpr int kChunk = 64;      // columns staged per round
+constexpr int kMaxSweeps = 30;  // Jacobi sweep cap (non-convergence is counted)
+
+// Round-robin ("circle") tournament in slot form: slots (2i, 2i+1) form pair i; slot 0 is
+// fixed and the other KP-1 slots rotate one ring position per step, so every pair of
+// indices meets exactly once per KP-1 steps and the slot permutation is the identity again
+// after a full sweep.
+template <int KP>
+struct Ring {
+  static constexpr int R = KP - 1;
+  // ring position of slot (slot != 0): tops 2i (i>=1) -> i-1, bottoms 2i+1 -> 2m-2-i
+  __host__ __device__ static constexpr int pos(int slot) {
+    return (slot & 1) ? (KP - 2 - (slot >> 1)) : ((slot >> 1) - 1);
+  }
+  __host__ __device__ static constexpr int slot_at(int p) {
+    return p < KP / 2 - 1 ? 2 * (p + 1) : 2 * (KP - 2 - p) + 1;
+  }
+  // index (player) sitting in `slot` at step s of a sweep
+  __host__ __device__ static int player(int slot, int s) {
+    if (slot == 0) return 0;
+    int p = pos(slot) - s;
+    p += p < 0 ? R : 0;
+    return slot_at(p);
+  }
+};
+
+template <int KP>
+struct SolveSmem {
+  union {
+    double A[KP][KP + 1];  // work matrix / eigenvectors at the end
+    struct {
+      float yb[kChunk][KP];
+      float yo[kChunk];
+      float w[kChunk];
+      int col[kChunk];
+    } ch;
+  } u;
+  double cs[KP / 2][4];  // c, s, t*apq per pair
+  double b1[KP];         // Yb d (fp64)
+  double xp[KP];         // x' = xb - xb_mean (fp64)
+  double z1[KP], z2[KP];
+  double lam[KP];
+  float xb[KP], xa[KP];
+  double scal[4];
+  float fscal[4];
+};
+
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  const int x = b & 7, l = b >> 3, q = n >> 3, r = n & 7;
+  return x * q + (x < r ? x : r) + l;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int KP, bool ASSEMBLED>
+__global__ void __launch_bounds__(64)
+solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, long long g0,
+             int npts, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
+             const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
+             const float *__restrict__ yo_in, const float *__restrict__ yb_in,
+             const float *__restrict__ xb_in, float *__restrict__ xa_out,
+             double *__restrict__ evals, int2 *__restrict__ info) {
+  static_assert(KP % 8 == 0 && KP <= 64, "KP");
+  constexpr int NB = KP / 4;                     // 4x4 blocks per dimension
+  constexpr int NBLK = NB * (NB + 1) / 2;        // lower-triangle blocks
+  constexpr int NBL = (NBLK + 63) / 64;          // blocks per lane
+  constexpr int NP = KP / 2;                     // pairs per step
+  constexpr int NPB = NP * (NP + 1) / 2;         // pair blocks (lower)
+  constexpr int NPL = (NPB + 63) / 64;
+  __shared__ SolveSmem<KP> sm;
+
+  const int gi = xcd_remap(blockIdx.x, gridDim.x);
+  if (gi >= npts) return;
+  const int lane = threadIdx.x;
+  const int k = c.k;
+
+  long long P = 0;  // var index of member 0
+  if constexpr (!ASSEMBLED) {
+    const long long g = g0 + gi;
+    const int i = (int)(g % slab.ix_lim);
+    const long long r = g / slab.ix_lim;
+    const int j = (int)(r % slab.iy_lim);
+    const int kz = (int)(r / slab.iy_lim);
+    P = i + (long long)slab.nx * (j + (long long)slab.ny * kz);
+    if (lane < KP) sm.xb[lane] = lane < k ? slab.var[P + slab.L * lane] : 0.0f;
+  } else {
+    if (lane < KP) sm.xb[lane] = lane < k ? xb_in[(long long)gi * k + lane] : 0.0f;
+  }
+
+  // ---- lane -> 4x4 block of the lower triangle of A --------------------------------
+  int bi[NBL], bj[NBL];
+#pragma unroll
+  for (int it = 0; it < NBL; ++it) {
+    const int b = lane + 64 * it;
+    int rr = 0;
+    while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;
+    bi[it] = rr;
+    bj[it] = b - rr * (rr + 1) / 2;
+  }
+  double acc[NBL][16];
+#pragma unroll
+  for (int it = 0; it < NBL; ++it)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[it][e] = 0.0;
+  double b1acc = 0.0;
+  int ptot = 0;
+
+  // accumulate nsl staged columns into A (lower) and Yb d
+  auto accumulate = [&](int nsl) {
+    for (int s = 0; s < nsl; ++s) {
+#pragma unroll
+      for (int it = 0; it < NBL; ++it) {
+        if (lane + 64 * it < NBLK) {
+          const float4 ra = *reinterpret_cast<const float4 *>(&sm.u.ch.yb[s][4 * bi[it]]);
+          const float4 rb = *reinterpret_cast<const float4 *>(&sm.u.ch.yb[s][4 * bj[it]]);
+          const double a4[4] = {ra.x, ra.y, ra.z, ra.w};
+          const double b4[4] = {rb.x, rb.y, rb.z, rb.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[it][4 * r + q] = fma(a4[r], b4[q], acc[it][4 * r + q]);
+        }
+      }
+      if (lane < KP) b1acc = fma((double)sm.u.ch.yb[s][lane], (double)sm.u.ch.yo[s], b1acc);
+    }
+  };
+
+  if constexpr (!ASSEMBLED) {
+    for (int t = 0; t < c.ntrees; ++t) {
+      const TreeDesc &T = trees[t];
+      const int cnt = nbr_cnt[(long long)gi * c.ntrees + t];
+      const int nvar = T.nvar;
+      const int npairs = cnt * nvar;
+      const long long lbase = (long long)gi * c.list_cap + T.list_off;
+      for (int base = 0; base < npairs; base += 64) {
+        const int q = base + lane;
+        bool ok = false;
+        int col = 0;
+        float w = 0.0f, yo = 0.0f;
+        if (q < npairs) {
+          const int jn = q / nvar, v = q - jn * nvar;
+          col = nbr_idx[lbase + jn] * nvar + v;
+          ok = T.col_ok[col] != 0;
+          if (ok) {
+            w = error_inv(c.weight_function, T.col_err[col], nbr_r2[lbase + jn]);
+            yo = T.col_omm[col] * w;  // omm * error_inv (:451)
+          }
+        }
+        const unsigned long long mask = __ballot(ok);
+        const int nsl = __popcll(mask);
+        if (ok) {
+          const int slot = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+          sm.u.ch.col[slot] = col;
+          sm.u.ch.w[slot] = w;
+          sm.u.ch.yo[slot] = yo;
+        }
+        __syncthreads();
+        if (nsl == 0) continue;
+        constexpr int V4 = KP / 4;
+        for (int e = lane; e < nsl * V4; e += 64) {
+          const int s = e / V4, c4 = e - s * V4;
+          const float4 g = reinterpret_cast<const float4 *>(T.col_bg + (long long)sm.u.ch.col[s] * KP)[c4];
+          const float ws = sm.u.ch.w[s];
+          float4 y;  // bg * error_inv (:452)
+          y.x = g.x * ws; y.y = g.y * ws; y.z = g.z * ws; y.w = g.w * ws;
+          *reinterpret_cast<float4 *>(&sm.u.ch.yb[s][4 * c4]) = y;
+        }
+        __syncthreads();
+        accumulate(nsl);
+        ptot += nsl;
+        __syncthreads();
+      }
+    }
+  } else {
+    const long long c0 = col_off[gi], c1 = col_off[gi + 1];
+    const int ncol = (int)(c1 - c0);
+    for (int base = 0; base < ncol; base += kChunk) {
+      const int nsl = min(kChunk, ncol - base);
+      if (lane < nsl) sm.u.ch.yo[lane] = yo_in[c0 + base + lane];
+      for (int e = lane; e < nsl * KP; e += 64) {
+        const int s = e / KP, m = e - s * KP;
+        sm.u.ch.yb[s][m] = m < k ? yb_in[(c0 + base + s) * k + m] : 0.0f;
+      }
+      __syncthreads();
+      accumulate(nsl);
+      ptot += nsl;
+      __syncthreads();
+    }
+  }
+
+  if (ptot == 0) {  // no accepted observation: var left unchanged (:220, :226)
+    if (lane == 0 && info) info[gi] = make_int2(0, 0);
+    if constexpr (ASSEMBLED) {
+      if (lane < k) xa_out[(long long)gi * k + lane] = sm.xb[lane];
+    }
+    return;
+  }
+
+  // ---- A = inflat*I + Yb Yb^T (full symmetric, padded identity) ----------------------
+  const double inflat_r8 = (double)c.inflat;
+#pragma unroll
+  for (int it = 0; it < NBL; ++it) {
+    if (lane + 64 * it < NBLK) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ii = 4 * bi[it] + r, jj = 4 * bj[it] + q;
+          double v = acc[it][4 * r + q];
+          if (ii == jj) v = ii < k ? v + inflat_r8 : 1.0;
+          sm.u.A[ii][jj] = v;
+          sm.u.A[jj][ii] = v;
+        }
+    }
+  }
+  if (lane < KP) sm.b1[lane] = b1acc;
+  if (lane == 0) {  // xb_mean = sum(xb) * nmember_inv in fp32 (:671)
+    float s = 0.0f;
+    for (int m = 0; m < k; ++m) s = s + sm.xb[m];
+    sm.scal[0] = (double)(s * c.nmember_inv);
+  }
+  __syncthreads();
+  const double xb_mean = sm.scal[0];
+  if (lane < KP) sm.xp[lane] = lane < k ? (double)sm.xb[lane] - xb_mean : 0.0;
+
+  // ---- parallel cyclic Jacobi ---------------------------------------------------------
+  double v[KP];  // row `lane` of V, column slots in ring order
+#pragma unroll
+  for (int q = 0; q < KP; ++q) v[q] = lane == q ? 1.0 : 0.0;
+  int pbP[NPL], pbQ[NPL];
+#pragma unroll
+  for (int it = 0; it < NPL; ++it) {
+    const int b = lane + 64 * it;
+    int rr = 0;
+    while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;
+    pbP[it] = rr;
+    pbQ[it] = b - rr * (rr + 1) / 2;
+  }
+  const double tol2 = 1e-28;  // rotate iff apq^2 > tol^2 * app * aqq, tol = 1e-14
+  int sweeps = 0;
+  bool converged = false;
+  for (int sweep = 0; sweep < kMaxSweeps; ++sweep) {
+    bool rotated = false;
+#pragma unroll 1
+    for (int st = 0; st < KP - 1; ++st) {
+      // rotation parameters of the NP disjoint pairs
+      if (lane < NP) {
+        const int p = Ring<KP>::player(2 * lane, st), q = Ring<KP>::player(2 * lane + 1, st);
+        const double app = sm.u.A[p][p], aqq = sm.u.A[q][q], apq = sm.u.A[p][q];
+        double cc = 1.0, ss = 0.0, tapq = 0.0;
+        if (apq != 0.0 && apq * apq > tol2 * fabs(app * aqq)) {
+          const double theta = (aqq - app) / (2.0 * apq);
+          double t;
+          if (fabs(theta) > 1e150) {
+            t = 0.5 / theta;
+          } else {
+            t = 1.0 / (fabs(theta) + sqrt(fma(theta, theta, 1.0)));
+            if (theta < 0.0) t = -t;
+          }
+          cc = 1.0 / sqrt(fma(t, t, 1.0));
+          ss = t * cc;
+          tapq = t * apq;
+          rotated = true;
+        }
+        sm.cs[lane][0] = cc;
+        sm.cs[lane][1] = ss;
+        sm.cs[lane][2] = tapq;
+      }
+      __syncthreads();
+      // A <- J^T A J on 2x2 blocks (pair P rows, pair Q columns), both triangles
+#pragma unroll
+      for (int it = 0; it < NPL; ++it) {
+        if (lane + 64 * it < NPB) {
+          const int PP = pbP[it], QQ = pbQ[it];
+          const int p1 = Ring<KP>::player(2 * PP, st), q1 = Ring<KP>::player(2 * PP + 1, st);
+          const double c1 = sm.cs[PP][0], s1 = sm.cs[PP][1];
+          if (PP == QQ) {
+            const double tapq = sm.cs[PP][2];
+            if (s1 != 0.0) {
+              sm.u.A[p1][p1] -= tapq;
+              sm.u.A[q1][q1] += tapq;
+              sm.u.A[p1][q1] = 0.0;
+              sm.u.A[q1][p1] = 0.0;
+            }
+          } else {
+            const int p2 = Ring<KP>::player(2 * QQ, st), q2 = Ring<KP>::player(2 * QQ + 1, st);
+            const double c2 = sm.cs[QQ][0], s2 = sm.cs[QQ][1];
+            if (s1 != 0.0 || s2 != 0.0) {
+              const double x = sm.u.A[p1][p2], y = sm.u.A[p1][q2];
+              const double z = sm.u.A[q1][p2], w = sm.u.A[q1][q2];
+              // rows: (J^T A)
+              const double x1 = fma(c1, x, -s1 * z), z1 = fma(s1, x, c1 * z);
+              const double y1 = fma(c1, y, -s1 * w), w1 = fma(s1, y, c1 * w);
+              // columns: (. J)
+              const double x2 = fma(c2, x1, -s2 * y1), y2 = fma(s2, x1, c2 * y1);
+              const double z2 = fma(c2, z1, -s2 * w1), w2 = fma(s2, z1, c2 * w1);
+              sm.u.A[p1][p2] = x2; sm.u.A[p1][q2] = y2;
+              sm.u.A[q1][p2] = z2; sm.u.A[q1][q2] = w2;
+              sm.u.A[p2][p1] = x2; sm.u.A[q2][p1] = y2;
+              sm.u.A[p2][q1] = z2; sm.u.A[q2][q1] = w2;
+            }
+          }
+        }
+      }
+      // V <- V J: slots (2i, 2i+1) hold pair i (in place) ...
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const double ci = sm.cs[i][0], si = sm.cs[i][1];
+        const double vp = v[2 * i], vq = v[2 * i + 1];
+        v[2 * i] = fma(ci, vp, -si * vq);
+        v[2 * i + 1] = fma(si, vp, ci * vq);
+      }
+      // ... then the ring advances: the index in ring position p moves to p+1 (one cycle
+      // over the KP-1 slots != 0, done in place with one temporary)
+      {
+        constexpr int R = KP - 1;
+        const double last = v[Ring<KP>::slot_at(R - 1)];
+#pragma unroll
+        for (int p = R - 1; p >= 1; --p) v[Ring<KP>::slot_at(p)] = v[Ring<KP>::slot_at(p - 1)];
+        v[Ring<KP>::slot_at(0)] = last;
+      }
+      __syncthreads();
+    }
+    sweeps = sweep + 1;
+    if (!__any(rotated)) { converged = true; break; }
+  }
+
+  // ---- apply the weights matrix-free ----------------------------------------------------
+  // eigenvalues lam_j = A(j,j); V written to LDS (A no longer needed)
+  if (lane < KP) sm.lam[lane] = sm.u.A[lane][lane];
+  __syncthreads();
+  if (lane < KP) {
+#pragma unroll
+    for (int q = 0; q < KP; ++q) sm.u.A[lane][q] = v[q];
+  }
+  __syncthreads();
+  if (lane < KP) {
+    double u1 = 0.0, u2 = 0.0;
+    for (int r = 0; r < KP; ++r) {
+      const double vr = sm.u.A[r][lane];
+      u1 = fma(vr, sm.b1[r], u1);   // V^T (Yb d)
+      u2 = fma(vr, sm.xp[r], u2);   // V^T x'
+    }
+    const double einv = 1.0 / sm.lam[lane];  // eval = 1/lambda (module_eigen.f90:52)
+    sm.z1[lane] = u1 * einv;
+    sm.z2[lane] = u2 * sqrt(einv);           // sqrt(eval) (module_eigen.f90:90)
+  }
+  __syncthreads();
+  double wb = 0.0, sr = 0.0;  // wbar_r = (Pa Yb d)_r ; s_r = (Pa^{1/2} x')_r
+#pragma unroll
+  for (int q = 0; q < KP; ++q) {
+    wb = fma(v[q], sm.z1[q], wb);
+    sr = fma(v[q], sm.z2[q], sr);
+  }
+  const double xpl = lane < KP ? sm.xp[lane] : 0.0;
+  const double d = wave_sum_f64(lane < k ? wb * xpl : 0.0);  // sum_i wbar_i x'_i
+  const double sk = sqrt((double)(k - 1));
+  if (lane < KP) sm.xa[lane] = (float)(xb_mean + (d + sk * sr));  // xa = wbar (:675-679)
+  __syncthreads();
+
+  // ---- RTPP / RTPS (:684-698), fp32 in the reference's order -------------------------
+  if (c.use_rtpp || c.use_rtps) {
+    if (lane == 0) {
+      float s = 0.0f;
+      for (int m = 0; m < k; ++m) s = s + sm.xa[m];
+      sm.fscal[0] = s * c.nmember_inv;  // xa_mean
+    }
+    __syncthreads();
+    const float xa_mean = sm.fscal[0];
+    float xap = 0.0f;
+    if (lane < k) {
+      xap = sm.xa[lane] - xa_mean;
+      if (c.use_rtpp)
+        xap = (float)((double)((1.0f - c.rtpp_alpha) * xap) + (double)c.rtpp_alpha * sm.xp[lane]);
+    }
+    if (c.use_rtps) {
+      __syncthreads();
+      if (lane < k) sm.xa[lane] = xap;  // stage xa_prime
+      __syncthreads();
+      if (lane == 0) {
+        double d8 = 0.0;
+        for (int m = 0; m < k; ++m) d8 = d8 + sm.xp[m] * sm.xp[m];
+        const float xb_std = (float)d8;
+        float xa_std = 0.0f;
+        for (int m = 0; m < k; ++m) xa_std = xa_std + sm.xa[m] * sm.xa[m];
+        sm.fscal[1] = c.rtps_alpha * sqrtf(xb_std / xa_std) - c.rtps_alpha + 1.0f;
+      }
+      __syncthreads();
+      xap = xap * sm.fscal[1];
+    }
+    if (lane < k) sm.xa[lane] = xa_mean + xap;
+    __syncthreads();
+  }
+
+  if (lane < k) {
+    if constexpr (ASSEMBLED) xa_out[(long long)gi * k + lane] = sm.xa[lane];
+    else slab.var[P + slab.L * lane] = sm.xa[lane];
+  }
+  if (lane == 0 && info) info[gi] = make_int2(ptot, converged ? sweeps : -sweeps);
+  if (ASSEMBLED && evals != nullptr && lane < k) {
+    // eigenvalues ascending (dsyevd order) over the k real indices
+    const double lj = sm.lam[lane];
+    int rank = 0;
+    for (int i = 0; i < k; ++i) {
+      const double li = sm.lam[i];
+      rank += (li < lj || (li == lj && i < lane)) ? 1 : 0;
+    }
+    evals[(long long)gi * k + rank] = lj;
+  }
+}
+
+template <int KP>
+static hipError_t launch_solve_kp(hipStream_t s, bool assembled, const TreeDesc *trees,
+                                  SolveConsts c, SlabDev slab, long long g0, int npts,
+                                  const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                                  const long long *col_off, const float *yo, const float *yb,
+                                  const float *xb, float *xa, double *evals, int2 *info) {
+  if (assembled)
+    hipLaunchKernelGGL((solve_kernel<KP, true>), dim3(npts), dim3(64), 0, s, trees, c, slab,
+                       g0, npts, nbr_cnt, nbr_idx, nbr_r2, col_off, yo, yb, xb, xa, evals, info);
+  else
+    hipLaunchKernelGGL((solve_kernel<KP, false>), dim3(npts), dim3(64), 0, s, trees, c, slab,
+                       g0, npts, nbr_cnt, nbr_idx, nbr_r2, col_off, yo, yb, xb, xa, evals, info);
+  return hipGetLastError();
+}
+
+static const int kSupportedKP[] = {8, 16, 24, 32, 40, 48, 56, 64};
+
+int supported_kp(int k) {
+  for (int kp : kSupportedKP)
+    if (k <= kp) return kp;
+  return -1;
+}
+
+static hipError_t dispatch_solve(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,
+                                 SolveConsts c, SlabDev slab, long long g0, int npts,
+                                 const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                                 const long long *col_off, const float *yo, const float *yb,
+                                 const float *xb, float *xa, double *evals, int2 *info) {
+  if (npts <= 0) return hipSuccess;
+#define CWBL_KP_CASE(K)                                                                      \
+  case K:                                                                                    \
+    return launch_solve_kp<K>(s, assembled, trees, c, slab, g0, npts, nbr_cnt, nbr_idx,      \
+                              nbr_r2, col_off, yo, yb, xb, xa, evals, info);
+  switch (kp) {
+    CWBL_KP_CASE(8)
+    CWBL_KP_CASE(16)
+    CWBL_KP_CASE(24)
+    CWBL_KP_CASE(32)
+    CWBL_KP_CASE(40)
+    CWBL_KP_CASE(48)
+    CWBL_KP_CASE(56)
+    CWBL_KP_CASE(64)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef CWBL_KP_CASE
+}
+
+hipError_t launch_solve_neighbors(hipStream_t s, int kp, const TreeDesc *trees,
+                                  SolveConsts c, SlabDev slab, long long g0, int npts,
+                                  const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                                  int2 *info) {
+  return dispatch_solve(s, kp, false, trees, c, slab, g0, npts, nbr_cnt, nbr_idx, nbr_r2,
+                        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, info);
+}
+
+hipError_t launch_solve_assembled(hipStream_t s, int kp, SolveConsts c, int npts,
+                                  const long long *col_off, const float *yo, const float *yb,
+                                  const float *xb, float *xa, double *evals, int2 *info) {
+  SlabDev none{};
+  return dispatch_solve(s, kp, true, nullptr, c, none, 0, npts, nullptr, nullptr, nullptr,
+                        col_off, yo, yb, xb, xa, evals, info);
+}
+
+// per-batch reduction of the per-point info into DevStats
+__global__ void __launch_bounds__(256)
+reduce_info_kernel(const int2 *__restrict__ info, int n, DevStats *stats) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  unsigned long long solved = 0, nobs = 0, noncv = 0;
+  unsigned int maxp = 0, maxsw = 0;
+  if (i < n) {
+    const int2 v = info[i];
+    if (v.x > 0) {
+      solved = 1;
+      nobs = (unsigned long long)v.x;
+      maxp = (unsigned)v.x;
+      const int sw = v.y < 0 ? -v.y : v.y;
+      maxsw = (unsigned)sw;
+      noncv = v.y < 0 ? 1 : 0;
+    }
+  }
+  // wave reductions, one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) {
+    solved += __shfl_xor(solved, off, 64);
+    nobs += __shfl_xor(nobs, off, 64);
+    noncv += __shfl_xor(noncv, off, 64);
+    maxp = max(maxp, (unsigned)__shfl_xor((int)maxp, off, 64));
+    maxsw = max(maxsw, (unsigned)__shfl_xor((int)maxsw, off, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (solved) atomicAdd(&stats->solved, solved);
+    if (nobs) atomicAdd(&stats->nobs_sum, nobs);
+    if (noncv) atomicAdd(&stats->nonconverged, noncv);
+    if (maxp) atomicMax(&stats->max_p, maxp);
+    if (maxsw) atomicMax(&stats->max_sweeps, maxsw);
+  }
+}
+
+hipError_t launch_reduce_info(hipStream_t s, const int2 *info, int n, DevStats *stats) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(reduce_info_kernel, dim3((n + 255) / 256), dim3(256), 0, s, info, n,
+                     stats);
+  return hipGetLastError();
+}
+
+}  // namespace cwbl

@@ -1,0 +1,122 @@
+"""Synthetic LETKF workloads of BASELINE.json's configs.
+
+All arrays are float32 numpy in the reference's Fortran layouts expressed as C-order
+shapes (see abi.py): x,y (ny,nx); alt (nz,ny,nx); var (k,nz,ny,nx); radar xyz (n,3),
+obs (n,), hdxb (k,n).  Data are synthetic (there is no network and the reference ships no
+sample data): a smooth "truth" field, member states xb = truth + N(0,1), observations
+obs = truth + N(0,1), simulated H(x_b) = truth + N(0, 2).
+"""
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+
+# name: (nx, ny, nz, k, n_obs, hclr_km, vclr_km, obs_ztop_m, radar type, err, err_rej, max_lz)
+CONFIGS = {
+    # configs[1]: 300x300x50 grid, k=40, ~200 local obs/point, single MI355X
+    "c2": dict(nx=300, ny=300, nz=50, k=40, n_obs=12300, hclr=12.0, vclr=3.0,
+               obs_ztop=15e3, radar_type=abi.RADAR_VR, err=1.0, err_rej=8.0, max_lz=1000),
+    # configs[3]: k=128 variant (needs the k>64 kernels; not in the v1 build)
+    "c4": dict(nx=300, ny=300, nz=50, k=128, n_obs=12300, hclr=12.0, vclr=3.0,
+               obs_ztop=15e3, radar_type=abi.RADAR_VR, err=1.0, err_rej=8.0, max_lz=1000),
+    # configs[4]: dense radar, 600x600x60, ~2000 local obs/point
+    "c5": dict(nx=600, ny=600, nz=60, k=40, n_obs=1_660_000, hclr=8.0, vclr=2.0,
+               obs_ztop=15e3, radar_type=abi.RADAR_DBZ, err=2.5, err_rej=20.0, max_lz=4000),
+}
+
+
+@dataclass
+class Workload:
+    name: str
+    k: int
+    nx: int
+    ny: int
+    nz: int
+    x: np.ndarray
+    y: np.ndarray
+    alt: np.ndarray
+    var: np.ndarray
+    radar_type: int
+    obs_xyz: np.ndarray
+    obs: np.ndarray
+    hdxb: np.ndarray
+    vp: object = None
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def points(self):
+        return self.nx * self.ny * self.nz
+
+
+def _truth(x, y, z):
+    # smooth field with ~40 km structures
+    return (2.0 * np.sin(x / 41e3) * np.cos(y / 37e3) + 0.5 * np.cos(z / 3.3e3)).astype(np.float32)
+
+
+def radar_var_params(hclr, vclr, max_lz, err, err_rej, radar_type, multi_infl=1.6):
+    """input.nml defaults for the analysed variable: RTPP/RTPS on with alpha .95
+    (input.nml:162-168), Gaussian weighting; one radar type."""
+    tp = abi.type_params(use_it=1, max_lz_pts=max_lz, hclr=hclr, vclr=vclr, err_muti=err,
+                         err_rej=err_rej)
+    return abi.var_params(multi_infl=multi_infl, use_rtpp=1, rtpp_alpha=0.95, use_rtps=1,
+                          rtps_alpha=0.95, radar={radar_type: tp})
+
+
+def make(name="c2", seed=20261015, scale=None, rows=None, **over):
+    """Build a workload.  `scale` shrinks nx/ny (domain and obs count scale with it) for
+    tests; `rows` = (start, step) keeps grid rows j = start, start+step, ... (cyclic
+    sharding of the columns across ranks, like the reference's block-1 decomposition,
+    module_mpi_util.f90:73-188).  The obs set never depends on `rows`."""
+    cfg = dict(CONFIGS[name])
+    cfg.update(over)
+    if scale:
+        cfg["nx"] = max(4, int(round(cfg["nx"] * scale)))
+        cfg["ny"] = max(4, int(round(cfg["ny"] * scale)))
+        cfg["n_obs"] = max(8, int(round(cfg["n_obs"] * scale * scale)))
+    nx, ny, nz, k = cfg["nx"], cfg["ny"], cfg["nz"], cfg["k"]
+    dx = 2e3
+    rng = np.random.default_rng(seed)
+    # observations (radar-like, uniform in the domain, alt 0..obs_ztop)
+    n = cfg["n_obs"]
+    ext_x, ext_y = nx * dx, ny * dx
+    oxyz = np.empty((n, 3), np.float32)
+    oxyz[:, 0] = rng.uniform(0, ext_x, n)
+    oxyz[:, 1] = rng.uniform(0, ext_y, n)
+    oxyz[:, 2] = rng.uniform(0, cfg["obs_ztop"], n)
+    t_o = _truth(oxyz[:, 0], oxyz[:, 1], oxyz[:, 2])
+    obs = (t_o + rng.standard_normal(n).astype(np.float32)).astype(np.float32)
+    hdxb = (t_o[None, :] + 2.0 * rng.standard_normal((k, n), dtype=np.float32)).astype(np.float32)
+    # grid: 2 km spacing, 50 levels 0..20 km with small column-dependent jitter
+    jx = np.arange(nx, dtype=np.float64) * dx
+    jy = np.arange(ny, dtype=np.float64) * dx
+    X, Y = np.meshgrid(jx, jy)                        # (ny, nx)
+    lev = np.linspace(20.0, 20e3, nz)
+    alt = (lev[:, None, None] + 15.0 * np.sin(X / 9e3)[None] * np.cos(Y / 11e3)[None]).astype(np.float32)
+    tr = _truth(X[None].astype(np.float32), Y[None].astype(np.float32), alt)  # (nz,ny,nx)
+    var = np.empty((k, nz, ny, nx), np.float32)
+    for m in range(k):
+        var[m] = tr + rng.standard_normal((nz, ny, nx), dtype=np.float32)
+    x = X.astype(np.float32)
+    y = Y.astype(np.float32)
+    if rows is not None:
+        start, step = rows
+        sel = np.arange(start, ny, step)
+        x, y = x[sel].copy(), y[sel].copy()
+        alt = alt[:, sel].copy()
+        var = var[:, :, sel].copy()
+    vp = radar_var_params(cfg["hclr"], cfg["vclr"], cfg["max_lz"], cfg["err"], cfg["err_rej"],
+                          cfg["radar_type"])
+    return Workload(name=name, k=k, nx=nx, ny=x.shape[0], nz=nz, x=x, y=y, alt=alt, var=var,
+                    radar_type=cfg["radar_type"], obs_xyz=oxyz, obs=obs, hdxb=hdxb, vp=vp,
+                    extra=dict(cfg=cfg, seed=seed, rows=rows))
+
+
+def flops_per_point(k, p):
+    """Algorithmic flop count of one point:
+    F(k,p) = p k(k+1) + 9k^3 + 4k^3 + 8pk + 4k^2."""
+    return p * k * (k + 1) + 13 * k ** 3 + 8 * p * k + 4 * k * k
+
+
+def flops_total(k, solved, nobs_sum):
+    return nobs_sum * (k * (k + 1) + 8 * k) + solved * (13 * k ** 3 + 4 * k * k)

@@ -1,0 +1,188 @@
+"""GPU parity tests: the HIP core through the C ABI against the reference's golden vectors
+(tests/golden/, produced by the reference's own compiled code) and against the oracle.
+
+Tolerances (north_star / SURVEY.md §8(d)):
+  analysis increments  rms(xa_gpu - xa_ref) / rms(xa_ref - xb) <= 1e-6   (INCR_TOL)
+  eigenvalues          max |lam_gpu - lam_ref| / lam_ref        <= 1e-12  (EIG_TOL), ascending
+  neighbour search     bit-exact (same indices, same traversal order, same fp32 r2)
+"""
+import numpy as np
+import pytest
+
+from cwbl import abi
+from helpers import (DriverCase, golden, inflat_of, increment_rel_rms, oracle)
+
+pytestmark = pytest.mark.gpu
+
+INCR_TOL = 1e-6
+EIG_TOL = 1e-12
+
+_cores = {}
+
+
+def core(k, wf=0, norain=-5.0, q1=abi.Q1_REPLICATE):
+    """One library state per process: re-init when the configuration changes."""
+    key = (k, wf, norain, q1)
+    if _cores.get("key") != key:
+        if "core" in _cores:
+            _cores["core"].finalize()
+        _cores["core"] = abi.Core(k, device=0, weight_function=wf, norain_value=norain,
+                                  q1_mode=q1)
+        _cores["key"] = key
+    return _cores["core"]
+
+
+@pytest.mark.parametrize("k", [8, 40, 64])
+def test_solve_batch_matches_reference(k):
+    g = golden(f"solve_k{k}.npz")
+    c = core(k)
+    col = g["col_off"]
+    # group points that share the solve parameters
+    keys = list(zip(g["multi_infl"], g["use_rtpp"], g["use_rtps"], g["rtpp_alpha"], g["rtps_alpha"]))
+    worst, worst_eig = 0.0, 0.0
+    for key in sorted(set(keys)):
+        sel = [i for i, kk in enumerate(keys) if kk == key]
+        off = np.concatenate([[0], np.cumsum([col[i + 1] - col[i] for i in sel])]).astype(np.int64)
+        yo = np.concatenate([g["yo"][col[i]:col[i + 1]] for i in sel])
+        yb = np.concatenate([g["yb"][col[i] * k:col[i + 1] * k] for i in sel])
+        xb = np.stack([g["xb"][i] for i in sel])
+        infl, rp, sp, ra, sa = key
+        xa, ev = c.solve_batch(off, yo, yb, xb, inflat_of(k, infl), int(rp), float(ra), int(sp),
+                               float(sa), want_evals=True)
+        for n, i in enumerate(sel):
+            worst = max(worst, increment_rel_rms(xa[n], g["xa"][i], g["xb"][i]))
+            rel = np.max(np.abs(ev[n] - g["lam"][i]) / np.abs(g["lam"][i]))
+            worst_eig = max(worst_eig, rel)
+    assert worst <= INCR_TOL, worst
+    assert worst_eig <= EIG_TOL, worst_eig
+
+
+def test_k128_reports_unsupported():
+    with pytest.raises(abi.CwblError, match="UNSUPPORTED"):
+        abi.Core(128, device=0)
+    _cores.clear()
+
+
+SEARCHES = ["search_3d.npz", "search_3d_overflow.npz", "search_2d.npz",
+            "search_2d_overflow_dups.npz", "search_3d_small.npz", "search_3d_bucket.npz"]
+
+
+@pytest.mark.parametrize("name", SEARCHES)
+def test_search_matches_reference_order(name):
+    g = golden(name)
+    c = core(8)
+    nf, idx, r2 = c.search(g["obs_xyz"], float(g["hclr"]), float(g["vclr"]), int(g["max_lz"]),
+                           g["q_xyz"])
+    np.testing.assert_array_equal(nf, g["nfound"])
+    for q in range(len(nf)):
+        n = nf[q]
+        np.testing.assert_array_equal(idx[q, :n], g["idx"][q, :n])
+        np.testing.assert_array_equal(r2[q, :n].view(np.uint32), g["r2"][q, :n].view(np.uint32))
+
+
+DRIVERS = ["driver_c1.npz", "driver_mixed.npz", "driver_gc_k40.npz", "driver_2d.npz",
+           "driver_q1.npz", "driver_offset.npz"]
+
+
+@pytest.mark.parametrize("name", DRIVERS)
+def test_driver_variable_matches_reference(name):
+    case = DriverCase(name)
+    c = core(case.k, case.wf, case.norain)
+    c.set_obs(case.obs_set())
+    slab, var = case.slab()
+    st = c.analyze_var(case.vp, slab)
+    rel = increment_rel_rms(var, case.var_out, case.var_in)
+    assert rel <= INCR_TOL, rel
+    # untouched points stay bit-identical (no accepted obs / outside ix_lim, iy_lim)
+    untouched = np.all(case.var_out == case.var_in, axis=0)
+    np.testing.assert_array_equal(var[:, untouched], case.var_in[:, untouched])
+    assert st.solved == int(np.sum(~untouched))
+    assert st.nonconverged == 0
+
+
+def test_device_memory_path_equals_host_path():
+    torch = pytest.importorskip("torch")
+    case = DriverCase("driver_mixed.npz")
+    c = core(case.k, case.wf, case.norain)
+    dev = torch.device("cuda:0")
+    to_dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    c.set_obs(case.obs_set(memory=abi.MEM_DEVICE, to_device=to_dev))
+    x, y, alt = (to_dev(np.asarray(a, np.float32)) for a in (case.x, case.y, case.alt))
+    var = to_dev(np.asarray(case.var_in, np.float32).copy())
+    torch.cuda.synchronize()
+    slab = abi.make_slab(x, y, alt, var, case.ix_lim, case.iy_lim, memory=abi.MEM_DEVICE)
+    c.analyze_var(case.vp, slab)
+    got = var.cpu().numpy()
+    # host path on the same inputs
+    c.set_obs(case.obs_set())
+    hslab, hvar = case.slab()
+    c.analyze_var(case.vp, hslab)
+    np.testing.assert_array_equal(got.view(np.uint32), hvar.view(np.uint32))
+
+
+def test_analyze_before_set_obs_is_a_state_error():
+    c = abi.Core(8, device=0)
+    _cores.clear()
+    case = DriverCase("driver_c1.npz")
+    slab, _ = case.slab()
+    with pytest.raises(abi.CwblError, match="STATE"):
+        c.analyze_var(case.vp, slab)
+    c.finalize()
+
+
+def _radar_case_scaled(scale, seed=11, **over):
+    from cwbl import synth
+    return synth.make("c2", seed=seed, scale=scale, **over)
+
+
+def test_synthetic_c2_subdomain_vs_oracle():
+    """C2-shaped workload (k=40, p~200) on a 60x60x50 sub-grid: GPU vs the oracle."""
+    import ctypes as C
+    w = _radar_case_scaled(0.2)
+    c = core(w.k)
+    b = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb)
+    c.set_obs(b.build())
+    var = w.var.copy()
+    st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+    ref = w.var.copy()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    ost = abi.Stats()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(w.x, w.y, w.alt, ref)), 16, C.byref(ost))
+    assert rc == 0
+    assert st.solved == ost.solved and st.nobs_sum == ost.nobs_sum
+    rel = increment_rel_rms(var, ref, w.var)
+    assert rel <= INCR_TOL, rel
+    assert st.nonconverged == 0
+
+
+def test_c2_full_size_properties():
+    """Full C2 size (300x300x50, k=40): properties that do not need the oracle everywhere,
+    plus an oracle check on a column block."""
+    import ctypes as C
+    from cwbl import synth
+    w = synth.make("c2")
+    c = core(w.k)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    var = w.var.copy()
+    st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+    assert st.points == w.points
+    assert np.isfinite(var).all()
+    assert st.nonconverged == 0
+    mean_p = st.nobs_sum / max(st.solved, 1)
+    assert 60 <= mean_p <= 400, mean_p
+    # idempotence of the API on unchanged inputs: a second call on the same xb is identical
+    var2 = w.var.copy()
+    c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var2))
+    np.testing.assert_array_equal(var.view(np.uint32), var2.view(np.uint32))
+    # oracle on a 12x12 column block (all 50 levels) cut out of the same grid
+    j0, i0, nb = 140, 150, 12
+    sub = lambda a: np.ascontiguousarray(a[..., j0:j0 + nb, i0:i0 + nb])  # noqa: E731
+    ref = sub(w.var).copy()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(sub(w.x), sub(w.y), sub(w.alt), ref)),
+                                  16, C.byref(abi.Stats()))
+    assert rc == 0
+    rel = increment_rel_rms(sub(var), ref, sub(w.var))
+    assert rel <= INCR_TOL, rel
