@@ -187,6 +187,7 @@ def main():
                 "ms_search_per_step": ms_search / args.steps,
                 "ms_prep_per_step": sum(s.ms_prep for s in stats) / args.steps,
                 "max_sweeps": max(s.max_sweeps for s in stats),
+                "mean_sweeps": sum(s.sweeps_sum for s in stats) / max(solved, 1),
                 "nonconverged": sum(s.nonconverged for s in stats),
                 "obs_bcast_ms": bcast_ms,
             },

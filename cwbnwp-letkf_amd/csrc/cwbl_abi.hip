@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -283,6 +284,8 @@ SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps,
   c.rtps_alpha = rtps_a;
   c.nmember_inv = 1.0f / (float)S.k;
   c.r2 = search_r2();
+  c.max_sweeps = 30;
+  if (const char *e = std::getenv("CWBL_DEBUG_MAX_SWEEPS")) c.max_sweeps = std::atoi(e);
   return c;
 }
 
@@ -515,6 +518,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   st.nobs_sum = (long long)ds.nobs_sum;
   st.lz_truncated = (long long)ds.lz_truncated;
   st.nonconverged = (long long)ds.nonconverged;
+  st.sweeps_sum = (long long)ds.sweeps_sum;
   st.max_p = (int)ds.max_p;
   st.max_sweeps = (int)ds.max_sweeps;
   st.ms_prep = elapsed(0, 1);

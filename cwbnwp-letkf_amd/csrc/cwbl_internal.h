@@ -65,6 +65,7 @@ struct SolveConsts {
   float inflat, rtpp_alpha, rtps_alpha;
   float nmember_inv;          // 1.0/k (module_param.f90:245)
   float r2;                   // gc1999**2
+  int   max_sweeps;           // Jacobi sweep cap (CWBL_DEBUG_MAX_SWEEPS overrides; ablation only)
 };
 
 // Point enumeration of a slab: g = i + ix_lim*(j + iy_lim*kz).
@@ -77,7 +78,7 @@ struct SlabDev {
 
 // Device-side counters (atomics) reported through cwbl_stats.
 struct DevStats {
-  unsigned long long solved, nobs_sum, lz_truncated, nonconverged, q1_undefined;
+  unsigned long long solved, nobs_sum, lz_truncated, nonconverged, q1_undefined, sweeps_sum;
   unsigned int max_p, max_sweeps;
 };
 

@@ -311,7 +311,7 @@ hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, float r2, i
 // solve_kernel<KP>: one wavefront (64 lanes) per grid point, members padded to KP
 // ---------------------------------------------------------------------------------------
 constexpr int kChunk = 64;      // columns staged per round
-constexpr int kMaxSweeps = 30;  // Jacobi sweep cap (non-convergence is counted)
+
 
 // Round-robin ("circle") tournament in slot form: slots (2i, 2i+1) form pair i; slot 0 is
 // fixed and the other KP-1 slots rotate one ring position per step, so every pair of
@@ -327,19 +327,35 @@ struct Ring {
   __host__ __device__ static constexpr int slot_at(int p) {
     return p < KP / 2 - 1 ? 2 * (p + 1) : 2 * (KP - 2 - p) + 1;
   }
-  // index (player) sitting in `slot` at step s of a sweep
-  __host__ __device__ static int player(int slot, int s) {
-    if (slot == 0) return 0;
-    int p = pos(slot) - s;
-    p += p < 0 ? R : 0;
-    return slot_at(p);
+  // slot the content of `slot` moves to after a step
+  __host__ __device__ static constexpr int next(int slot) {
+    return slot == 0 ? 0 : slot_at(pos(slot) + 1 == R ? 0 : pos(slot) + 1);
   }
 };
+
+// fp64 reciprocal / reciprocal square root: hardware estimate + two Newton steps (~1 ulp).
+// The rotation only needs c^2 + s^2 = 1 to working precision, not IEEE-rounded c and s.
+__device__ __forceinline__ double rcp64(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+__device__ __forceinline__ double rsq64(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double t = fma(-h * y, y, 0.5);
+  y = fma(y, t, y);
+  t = fma(-h * y, y, 0.5);
+  return fma(y, t, y);
+}
 
 template <int KP>
 struct SolveSmem {
   union {
-    double A[KP][KP + 1];  // work matrix / eigenvectors at the end
+    double A[KP + 1][KP + 2];  // work matrix (16-B aligned rows; last row = dummy
+                               // target of padding writes) / eigenvectors at the end
     struct {
       float yb[kChunk][KP];
       float yo[kChunk];
@@ -347,7 +363,7 @@ struct SolveSmem {
       int col[kChunk];
     } ch;
   } u;
-  double cs[KP / 2][4];  // c, s, t*apq per pair
+  double cs[KP / 2][2];  // c, s per pair
   double b1[KP];         // Yb d (fp64)
   double xp[KP];         // x' = xb - xb_mean (fp64)
   double z1[KP], z2[KP];
@@ -540,94 +556,112 @@ solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, lo
   if (lane < KP) sm.xp[lane] = lane < k ? (double)sm.xb[lane] - xb_mean : 0.0;
 
   // ---- parallel cyclic Jacobi ---------------------------------------------------------
-  double v[KP];  // row `lane` of V, column slots in ring order
+  // Brent-Luk ordering in "slot" space: slots (2i, 2i+1) are pair i of every step and, after
+  // a step, the content of slot s moves to Ring::next(s) (circle tournament, identity after
+  // KP-1 steps).  Every lane owns fixed 2x2 blocks (P,Q), P >= Q, of the lower triangle in
+  // slot space, held in registers; the step's permutation is a write of each element to its
+  // new (static) LDS position and a read-back.  V (row `lane`) lives in VGPRs in slot order.
+  constexpr int LD = KP + 2;
+  double *M = &sm.u.A[0][0];
+  double v[KP];
 #pragma unroll
   for (int q = 0; q < KP; ++q) v[q] = lane == q ? 1.0 : 0.0;
-  int pbP[NPL], pbQ[NPL];
+  int bP[NPL], bQ[NPL], wad[NPL][4], rad[NPL];
+  double e[NPL][4];
+  constexpr int DUMMY = KP * LD;  // LDS element that absorbs writes of padding lanes
 #pragma unroll
   for (int it = 0; it < NPL; ++it) {
     const int b = lane + 64 * it;
-    int rr = 0;
-    while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;
-    pbP[it] = rr;
-    pbQ[it] = b - rr * (rr + 1) / 2;
+    const bool valid = b < NPB;
+    int PP = 0, QQ = 0;
+    if (b < NP) {
+      PP = QQ = b;  // diagonal blocks first: lanes 0..NP-1 of it = 0
+    } else if (valid) {
+      const int bb = b - NP;
+      int rr = 0;
+      while ((rr + 1) * (rr + 2) / 2 <= bb) ++rr;
+      PP = rr + 1;
+      QQ = bb - rr * (rr + 1) / 2;
+    }
+    bP[it] = PP;
+    bQ[it] = QQ;
+    const int rs[4] = {2 * PP, 2 * PP, 2 * PP + 1, 2 * PP + 1};
+    const int cl[4] = {2 * QQ, 2 * QQ + 1, 2 * QQ, 2 * QQ + 1};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int nr = Ring<KP>::next(rs[j]), nc = Ring<KP>::next(cl[j]);
+      if (nr < nc) { const int t = nr; nr = nc; nc = t; }
+      wad[it][j] = (!valid || (PP == QQ && j == 1)) ? DUMMY + j : nr * LD + nc;
+    }
+    rad[it] = 2 * PP * LD + 2 * QQ;
+    const double2 r0 = *reinterpret_cast<const double2 *>(M + rad[it]);
+    const double2 r1 = *reinterpret_cast<const double2 *>(M + rad[it] + LD);
+    e[it][0] = r0.x; e[it][1] = PP == QQ ? r1.x : r0.y; e[it][2] = r1.x; e[it][3] = r1.y;
   }
-  const double tol2 = 1e-28;  // rotate iff apq^2 > tol^2 * app * aqq, tol = 1e-14
+  const bool diag_lane = lane < NP;  // owns diagonal block (lane,lane) as e[0]
+  const double tol = 1e-14;   // rotate pair (p,q) iff |apq| > tol * sqrt(app*aqq)
+  const double tol_q = 1e-8;  // quadratic convergence: a sweep that started below this ends ~1e-16
   int sweeps = 0;
   bool converged = false;
-  for (int sweep = 0; sweep < kMaxSweeps; ++sweep) {
+  for (int sweep = 0; sweep < c.max_sweeps; ++sweep) {
     bool rotated = false;
+    double mrel = 0.0;
 #pragma unroll 1
     for (int st = 0; st < KP - 1; ++st) {
-      // rotation parameters of the NP disjoint pairs
-      if (lane < NP) {
-        const int p = Ring<KP>::player(2 * lane, st), q = Ring<KP>::player(2 * lane + 1, st);
-        const double app = sm.u.A[p][p], aqq = sm.u.A[q][q], apq = sm.u.A[p][q];
-        double cc = 1.0, ss = 0.0, tapq = 0.0;
-        if (apq != 0.0 && apq * apq > tol2 * fabs(app * aqq)) {
-          const double theta = (aqq - app) / (2.0 * apq);
-          double t;
-          if (fabs(theta) > 1e150) {
-            t = 0.5 / theta;
-          } else {
-            t = 1.0 / (fabs(theta) + sqrt(fma(theta, theta, 1.0)));
-            if (theta < 0.0) t = -t;
-          }
-          cc = 1.0 / sqrt(fma(t, t, 1.0));
-          ss = t * cc;
-          tapq = t * apq;
-          rotated = true;
+      // rotation parameters from the diagonal blocks (lane P < NP owns block (P,P)),
+      // computed branch-free on every lane and published by the diagonal lanes
+      double d0, d3, cc = 1.0, ss = 0.0;
+      bool rot = false;
+      {
+        const double app = e[0][0], aqq = e[0][3], apq = e[0][2];
+        const double rel = fabs(apq) * rsq64(app * aqq);
+        rot = diag_lane && apq != 0.0 && rel > tol;
+        mrel = diag_lane && apq != 0.0 ? fmax(mrel, rel) : mrel;
+        const double theta = (aqq - app) * rcp64(2.0 * apq);
+        const double w = fma(theta, theta, 1.0);
+        double t = fabs(theta) > 1e150 ? 0.5 * rcp64(fabs(theta))
+                                       : rcp64(fabs(theta) + w * rsq64(w));
+        t = theta < 0.0 ? -t : t;
+        const double c0 = rsq64(fma(t, t, 1.0));
+        cc = rot ? c0 : 1.0;
+        ss = rot ? t * c0 : 0.0;
+        const double tapq = rot ? t * apq : 0.0;
+        d0 = app - tapq;
+        d3 = aqq + tapq;
+        rotated |= rot;
+        if (diag_lane) {
+          sm.cs[lane][0] = cc;
+          sm.cs[lane][1] = ss;
         }
-        sm.cs[lane][0] = cc;
-        sm.cs[lane][1] = ss;
-        sm.cs[lane][2] = tapq;
       }
       __syncthreads();
-      // A <- J^T A J on 2x2 blocks (pair P rows, pair Q columns), both triangles
+      // all blocks: rows rotated by pair P, columns by pair Q
 #pragma unroll
       for (int it = 0; it < NPL; ++it) {
-        if (lane + 64 * it < NPB) {
-          const int PP = pbP[it], QQ = pbQ[it];
-          const int p1 = Ring<KP>::player(2 * PP, st), q1 = Ring<KP>::player(2 * PP + 1, st);
-          const double c1 = sm.cs[PP][0], s1 = sm.cs[PP][1];
-          if (PP == QQ) {
-            const double tapq = sm.cs[PP][2];
-            if (s1 != 0.0) {
-              sm.u.A[p1][p1] -= tapq;
-              sm.u.A[q1][q1] += tapq;
-              sm.u.A[p1][q1] = 0.0;
-              sm.u.A[q1][p1] = 0.0;
-            }
-          } else {
-            const int p2 = Ring<KP>::player(2 * QQ, st), q2 = Ring<KP>::player(2 * QQ + 1, st);
-            const double c2 = sm.cs[QQ][0], s2 = sm.cs[QQ][1];
-            if (s1 != 0.0 || s2 != 0.0) {
-              const double x = sm.u.A[p1][p2], y = sm.u.A[p1][q2];
-              const double z = sm.u.A[q1][p2], w = sm.u.A[q1][q2];
-              // rows: (J^T A)
-              const double x1 = fma(c1, x, -s1 * z), z1 = fma(s1, x, c1 * z);
-              const double y1 = fma(c1, y, -s1 * w), w1 = fma(s1, y, c1 * w);
-              // columns: (. J)
-              const double x2 = fma(c2, x1, -s2 * y1), y2 = fma(s2, x1, c2 * y1);
-              const double z2 = fma(c2, z1, -s2 * w1), w2 = fma(s2, z1, c2 * w1);
-              sm.u.A[p1][p2] = x2; sm.u.A[p1][q2] = y2;
-              sm.u.A[q1][p2] = z2; sm.u.A[q1][q2] = w2;
-              sm.u.A[p2][p1] = x2; sm.u.A[q2][p1] = y2;
-              sm.u.A[p2][q1] = z2; sm.u.A[q2][q1] = w2;
-            }
-          }
-        }
+        const double2 p1 = *reinterpret_cast<const double2 *>(&sm.cs[bP[it]][0]);
+        const double2 p2 = *reinterpret_cast<const double2 *>(&sm.cs[bQ[it]][0]);
+        const double c1 = p1.x, s1 = p1.y, c2 = p2.x, s2 = p2.y;
+        const double x = e[it][0], y = e[it][1], z = e[it][2], w = e[it][3];
+        const double x1 = fma(c1, x, -s1 * z), z1 = fma(s1, x, c1 * z);
+        const double y1 = fma(c1, y, -s1 * w), w1 = fma(s1, y, c1 * w);
+        e[it][0] = fma(c2, x1, -s2 * y1);
+        e[it][1] = fma(s2, x1, c2 * y1);
+        e[it][2] = fma(c2, z1, -s2 * w1);
+        e[it][3] = fma(s2, z1, c2 * w1);
       }
-      // V <- V J: slots (2i, 2i+1) hold pair i (in place) ...
+      // diagonal blocks take the exact Jacobi update (a'_pp = app - t apq, a'_pq = 0)
+      e[0][0] = diag_lane ? d0 : e[0][0];
+      e[0][3] = diag_lane ? d3 : e[0][3];
+      e[0][1] = diag_lane && rot ? 0.0 : e[0][1];
+      e[0][2] = diag_lane && rot ? 0.0 : e[0][2];
+      // V <- V J on the slot pairs, then the ring advance of the slots
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
-        const double ci = sm.cs[i][0], si = sm.cs[i][1];
+        const double2 pc = *reinterpret_cast<const double2 *>(&sm.cs[i][0]);
         const double vp = v[2 * i], vq = v[2 * i + 1];
-        v[2 * i] = fma(ci, vp, -si * vq);
-        v[2 * i + 1] = fma(si, vp, ci * vq);
+        v[2 * i] = fma(pc.x, vp, -pc.y * vq);
+        v[2 * i + 1] = fma(pc.y, vp, pc.x * vq);
       }
-      // ... then the ring advances: the index in ring position p moves to p+1 (one cycle
-      // over the KP-1 slots != 0, done in place with one temporary)
       {
         constexpr int R = KP - 1;
         const double last = v[Ring<KP>::slot_at(R - 1)];
@@ -635,10 +669,27 @@ solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, lo
         for (int p = R - 1; p >= 1; --p) v[Ring<KP>::slot_at(p)] = v[Ring<KP>::slot_at(p - 1)];
         v[Ring<KP>::slot_at(0)] = last;
       }
+      // permute A: every element to its new slot position (lower triangle)
+#pragma unroll
+      for (int it = 0; it < NPL; ++it)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) M[wad[it][j]] = e[it][j];
       __syncthreads();
+#pragma unroll
+      for (int it = 0; it < NPL; ++it) {
+        const double2 r0 = *reinterpret_cast<const double2 *>(M + rad[it]);
+        const double2 r1 = *reinterpret_cast<const double2 *>(M + rad[it] + LD);
+        e[it][0] = r0.x;
+        e[it][1] = (it == 0 && diag_lane) ? r1.x : r0.y;
+        e[it][2] = r1.x;
+        e[it][3] = r1.y;
+      }
     }
     sweeps = sweep + 1;
-    if (!__any(rotated)) { converged = true; break; }
+    const bool any_rot = __any(rotated);
+    double wm = mrel;
+    for (int off = 32; off > 0; off >>= 1) wm = fmax(wm, __shfl_xor(wm, off, 64));
+    if (!any_rot || wm < tol_q) { converged = true; break; }
   }
 
   // ---- apply the weights matrix-free ----------------------------------------------------
@@ -793,7 +844,7 @@ hipError_t launch_solve_assembled(hipStream_t s, int kp, SolveConsts c, int npts
 __global__ void __launch_bounds__(256)
 reduce_info_kernel(const int2 *__restrict__ info, int n, DevStats *stats) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  unsigned long long solved = 0, nobs = 0, noncv = 0;
+  unsigned long long solved = 0, nobs = 0, noncv = 0, swsum = 0;
   unsigned int maxp = 0, maxsw = 0;
   if (i < n) {
     const int2 v = info[i];
@@ -803,6 +854,7 @@ reduce_info_kernel(const int2 *__restrict__ info, int n, DevStats *stats) {
       maxp = (unsigned)v.x;
       const int sw = v.y < 0 ? -v.y : v.y;
       maxsw = (unsigned)sw;
+      swsum = (unsigned long long)sw;
       noncv = v.y < 0 ? 1 : 0;
     }
   }
@@ -811,6 +863,7 @@ reduce_info_kernel(const int2 *__restrict__ info, int n, DevStats *stats) {
     solved += __shfl_xor(solved, off, 64);
     nobs += __shfl_xor(nobs, off, 64);
     noncv += __shfl_xor(noncv, off, 64);
+    swsum += __shfl_xor(swsum, off, 64);
     maxp = max(maxp, (unsigned)__shfl_xor((int)maxp, off, 64));
     maxsw = max(maxsw, (unsigned)__shfl_xor((int)maxsw, off, 64));
   }
@@ -818,6 +871,7 @@ reduce_info_kernel(const int2 *__restrict__ info, int n, DevStats *stats) {
     if (solved) atomicAdd(&stats->solved, solved);
     if (nobs) atomicAdd(&stats->nobs_sum, nobs);
     if (noncv) atomicAdd(&stats->nonconverged, noncv);
+    if (swsum) atomicAdd(&stats->sweeps_sum, swsum);
     if (maxp) atomicMax(&stats->max_p, maxp);
     if (maxsw) atomicMax(&stats->max_sweeps, maxsw);
   }

@@ -73,7 +73,8 @@ class Slab(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("points", C.c_longlong), ("solved", C.c_longlong), ("nobs_sum", C.c_longlong),
                 ("lz_truncated", C.c_longlong), ("nonconverged", C.c_longlong),
-                ("q1_undefined", C.c_longlong), ("max_p", C.c_int), ("max_sweeps", C.c_int),
+                ("q1_undefined", C.c_longlong), ("sweeps_sum", C.c_longlong),
+                ("max_p", C.c_int), ("max_sweeps", C.c_int),
                 ("ntrees", C.c_int), ("reserved", C.c_int), ("ms_total", C.c_double),
                 ("ms_prep", C.c_double), ("ms_search", C.c_double), ("ms_solve", C.c_double),
                 ("ms_copy", C.c_double)]
@@ -193,8 +194,23 @@ def default_library_path():
     return os.path.join(os.path.dirname(here), "lib", "libcwbl.so")
 
 
+def _share_torch_hip_runtime():
+    """PyTorch-ROCm wheels bundle their own libamdhip64 (same SONAME as /opt/rocm's).  If
+    libcwbl.so were loaded first, a later `import torch` would bring a second HIP/HSA runtime
+    into the process and torch would find no GPU.  Loading torch first makes the dynamic
+    loader bind libcwbl.so to torch's runtime, so one runtime serves both (device pointers
+    from torch tensors are then valid in the library).  Opt out: CWBL_NO_TORCH=1."""
+    if os.environ.get("CWBL_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load_library(path=None):
     """Load the product library; raises OSError when it has not been built."""
+    _share_torch_hip_runtime()
     lib = C.CDLL(path or os.environ.get("CWBL_LIBRARY") or default_library_path())
     vp, cp = C.c_void_p, C.c_char_p
     lib.cwbl_init.argtypes = [C.POINTER(InitParams)]

@@ -167,6 +167,7 @@ typedef struct cwbl_stats {
   long long nonconverged;    /* eigensolves that hit the sweep cap (LAPACK info ignored, */
                              /* module_eigen.f90:49) */
   long long q1_undefined;    /* (point, type) searches in the Q1 undefined case */
+  long long sweeps_sum;      /* Jacobi sweeps summed over solved points */
   int       max_p;           /* max p over points */
   int       max_sweeps;      /* max Jacobi sweeps used */
   int       ntrees;          /* trees built for this variable */

@@ -115,8 +115,17 @@ class DriverCase:
 
 
 def increment_rel_rms(xa, xa_ref, xb):
-    """SURVEY.md §8(d) parity metric: rms(xa - xa_ref) / rms(xa_ref - xb)."""
+    """SURVEY.md §8(d) parity metric: rms(xa - xa_ref) / rms(xa_ref - xb).
+
+    NaN-aware: the reference itself produces NaN analyses (Q8: with weight_function=1 the
+    fp32 Gaspari-Cohn polynomial returns tiny negatives near z=2 and sqrt() gives NaN,
+    module_localization.f90:360 / module_letkf_core.f90:449).  NaNs must occur at exactly
+    the same places; the metric is taken over the finite values."""
     xa, xa_ref, xb = (np.asarray(a, np.float64) for a in (xa, xa_ref, xb))
-    den = np.sqrt(np.mean((xa_ref - xb) ** 2))
-    num = np.sqrt(np.mean((xa - xa_ref) ** 2))
+    nan_a, nan_r = np.isnan(xa), np.isnan(xa_ref)
+    if not np.array_equal(nan_a, nan_r):
+        return float("inf")
+    fin = ~nan_r
+    den = np.sqrt(np.mean((xa_ref[fin] - xb[fin]) ** 2)) if fin.any() else 0.0
+    num = np.sqrt(np.mean((xa[fin] - xa_ref[fin]) ** 2)) if fin.any() else 0.0
     return num / den if den > 0 else num
