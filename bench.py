@@ -32,6 +32,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from cwbl import abi, synth  # noqa: E402
+from cwbl import dist as cdist  # noqa: E402
 
 METRIC = "analysis grid-points/sec (+ wall-clock per cycle) at k=40, 1/2/4/8 MI355X"
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector = matrix on gfx950), spec
@@ -89,20 +90,18 @@ def main():
     k = w.k
     # ---- observation set: generated on rank 0, one RCCL broadcast --------------------------
     n = w.obs.shape[0]
-    pack = torch.empty(n * (4 + k), dtype=torch.float32, device=dev)
+    pack = torch.empty(cdist.packed_len(n, k), dtype=torch.float32, device=dev)
     if rank == 0:
-        pack.copy_(torch.from_numpy(np.concatenate([w.obs_xyz.ravel(), w.obs, w.hdxb.ravel()])))
+        pack.copy_(torch.from_numpy(cdist.pack_radar(w.obs_xyz, w.obs, w.hdxb)))
     bcast_ms = 0.0
     if world > 1:
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        dist.broadcast(pack, src=0)
+        cdist.broadcast_obs(pack, src=0)
         torch.cuda.synchronize()
         bcast_ms = (time.perf_counter() - t0) * 1e3
-    oxyz = pack[:3 * n].view(n, 3)
-    oobs = pack[3 * n:4 * n]
-    ohdxb = pack[4 * n:].view(k, n)
+    oxyz, oobs, ohdxb = cdist.unpack_radar(pack, n, k)
     # ---- slab in HBM ---------------------------------------------------------------------------
     x, y, alt = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt))
     var = torch.from_numpy(w.var).to(dev)

@@ -102,8 +102,8 @@ def make(name="c2", seed=20261015, scale=None, rows=None, **over):
     x = X.astype(np.float32)
     y = Y.astype(np.float32)
     if rows is not None:
-        start, step = rows
-        sel = np.arange(start, ny, step)
+        from .dist import shard_rows
+        sel = shard_rows(ny, rows[0], rows[1])
         x, y = x[sel].copy(), y[sel].copy()
         alt = alt[:, sel].copy()
         var = var[:, :, sel].copy()

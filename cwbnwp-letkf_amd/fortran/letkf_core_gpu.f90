@@ -1,0 +1,153 @@
+! letkf_core_gpu.f90 — iso_c_binding interface to the MI355X LETKF core (include/cwb_letkf_core.h).
+!
+! This is the Fortran side of the drop-in boundary: the reference's letkf_driver
+! (module_letkf_core.f90:21-298) keeps its variable loop, scatter/gather and tune_q, and
+! replaces build_tree + the grid-point loop (:63-64, :209-240) by one call of
+! cwbl_analyze_var per variable (INTEGRATION.md shows the edited driver).
+!
+! Types mirror the C structs field by field (bind(C)); logicals cross as integer(c_int) 0/1.
+module letkf_core_gpu
+    use iso_c_binding
+    implicit none
+    private
+
+    integer(c_int), parameter, public :: CWBL_MEM_HOST = 0, CWBL_MEM_DEVICE = 1
+    integer(c_int), parameter, public :: CWBL_Q1_REPLICATE = 0, CWBL_Q1_PER_TYPE = 1
+    integer,        parameter, public :: CWBL_NUM_GTS_TYPES = 29, CWBL_NUM_RADAR_TYPES = 4
+
+    type, bind(C), public :: cwbl_init_params
+        integer(c_int)    :: nmember, device, weight_function
+        real(c_float)     :: norain_value
+        integer(c_int)    :: q1_mode, reserved
+        integer(c_size_t) :: workspace_bytes
+    end type cwbl_init_params
+
+    type, bind(C), public :: cwbl_gts_obs          ! type(gts_structure), module_gts_omboma.f90:13-22
+        integer(c_int) :: type_id, nvar, nobs, reserved
+        type(c_ptr)    :: xyz, obs, error, hdxb, qc
+    end type cwbl_gts_obs
+
+    type, bind(C), public :: cwbl_radar_obs        ! type(radar_structure), module_radar.f90:13-16
+        integer(c_int) :: type_id, nobs
+        type(c_ptr)    :: xyz, obs, hdxb
+    end type cwbl_radar_obs
+
+    type, bind(C), public :: cwbl_obs_set
+        integer(c_int) :: n_gts, n_radar
+        type(c_ptr)    :: gts, radar
+        integer(c_int) :: memory, reserved
+    end type cwbl_obs_set
+
+    type, bind(C), public :: cwbl_type_params      ! gts_config / radar_variable_config
+        integer(c_int) :: use_it, max_lz_pts
+        real(c_float)  :: hclr, vclr
+        real(c_float)  :: err_muti(5), err_rej(5)
+        integer(c_int) :: is_assim(5)
+    end type cwbl_type_params
+
+    type, bind(C), public :: cwbl_var_params
+        real(c_float)          :: multi_infl
+        integer(c_int)         :: use_rtpp
+        real(c_float)          :: rtpp_alpha
+        integer(c_int)         :: use_rtps
+        real(c_float)          :: rtps_alpha
+        integer(c_int)         :: reserved
+        type(cwbl_type_params) :: gts(CWBL_NUM_GTS_TYPES)
+        type(cwbl_type_params) :: radar(CWBL_NUM_RADAR_TYPES)
+    end type cwbl_var_params
+
+    type, bind(C), public :: cwbl_slab             ! var(nx,ny,nz,0:k-1), module_letkf_core.f90:85
+        integer(c_int) :: nx, ny, nz, alt_nx, alt_ny, ix_lim, iy_lim, memory
+        type(c_ptr)    :: x, y, alt, var
+    end type cwbl_slab
+
+    type, bind(C), public :: cwbl_stats
+        integer(c_long_long) :: points, solved, nobs_sum, lz_truncated, nonconverged, &
+                                q1_undefined, sweeps_sum
+        integer(c_int)       :: max_p, max_sweeps, ntrees, reserved
+        real(c_double)       :: ms_total, ms_prep, ms_search, ms_solve, ms_copy
+    end type cwbl_stats
+
+    public :: cwbl_init, cwbl_set_obs, cwbl_analyze_var, cwbl_solve_batch, cwbl_search, &
+              cwbl_finalize, cwbl_abi_version, cwbl_error, cwbl_check
+
+    interface
+        integer(c_int) function cwbl_init(p) bind(C, name='cwbl_init')
+            import :: c_int, cwbl_init_params
+            type(cwbl_init_params), intent(in) :: p
+        end function cwbl_init
+
+        integer(c_int) function cwbl_set_obs(o) bind(C, name='cwbl_set_obs')
+            import :: c_int, cwbl_obs_set
+            type(cwbl_obs_set), intent(in) :: o
+        end function cwbl_set_obs
+
+        integer(c_int) function cwbl_analyze_var(vp, slab, stats) bind(C, name='cwbl_analyze_var')
+            import :: c_int, cwbl_var_params, cwbl_slab, cwbl_stats
+            type(cwbl_var_params), intent(in)    :: vp
+            type(cwbl_slab),       intent(in)    :: slab
+            type(cwbl_stats),      intent(inout) :: stats
+        end function cwbl_analyze_var
+
+        integer(c_int) function cwbl_solve_batch(npts, col_off, yo, yb, xb, inflat, use_rtpp, &
+                rtpp_alpha, use_rtps, rtps_alpha, xa, evals, memory) bind(C, name='cwbl_solve_batch')
+            import :: c_int, c_float, c_ptr
+            integer(c_int), value :: npts, use_rtpp, use_rtps, memory
+            real(c_float),  value :: inflat, rtpp_alpha, rtps_alpha
+            type(c_ptr),    value :: col_off, yo, yb, xb, xa, evals
+        end function cwbl_solve_batch
+
+        integer(c_int) function cwbl_search(nobs, obs_xyz, hclr, vclr, max_lz_pts, nq, q_xyz, &
+                nfound, idx, r2, memory) bind(C, name='cwbl_search')
+            import :: c_int, c_float, c_ptr
+            integer(c_int), value :: nobs, max_lz_pts, nq, memory
+            real(c_float),  value :: hclr, vclr
+            type(c_ptr),    value :: obs_xyz, q_xyz, nfound, idx, r2
+        end function cwbl_search
+
+        integer(c_int) function cwbl_finalize() bind(C, name='cwbl_finalize')
+            import :: c_int
+        end function cwbl_finalize
+
+        integer(c_int) function cwbl_abi_version() bind(C, name='cwbl_abi_version')
+            import :: c_int
+        end function cwbl_abi_version
+
+        type(c_ptr) function cwbl_last_error_c() bind(C, name='cwbl_last_error')
+            import :: c_ptr
+        end function cwbl_last_error_c
+    end interface
+
+contains
+
+    ! cwbl_last_error() as a Fortran string
+    function cwbl_error() result(msg)
+        character(len=:), allocatable :: msg
+        type(c_ptr) :: p
+        character(kind=c_char), pointer :: s(:)
+        integer :: n
+        p = cwbl_last_error_c()
+        msg = ''
+        if (.not. c_associated(p)) return
+        call c_f_pointer(p, s, [4096])
+        n = 0
+        do while (n < 4096)
+            if (s(n+1) == c_null_char) exit
+            n = n + 1
+        end do
+        allocate(character(len=n) :: msg)
+        msg = transfer(s(1:n), msg)
+    end function cwbl_error
+
+    ! The reference's error convention: a failing call ends the program with `stop "<msg>"`
+    ! (module_config.f90:123-146, module_netcdf_io.f90:378-386).  The library itself never exits.
+    subroutine cwbl_check(rc, what)
+        integer(c_int),   intent(in) :: rc
+        character(len=*), intent(in) :: what
+        if (rc /= 0) then
+            print '(a,a,i0,a,a)', what, ' failed, code ', rc, ': ', cwbl_error()
+            stop "LETKF core error"
+        end if
+    end subroutine cwbl_check
+
+end module letkf_core_gpu

@@ -1,0 +1,89 @@
+"""Multi-process (world_size 2, gloo, CPU) check of the sharded path: rows dealt cyclically,
+the obs set broadcast once from rank 0, each rank analysing its shard independently (with
+the oracle standing in for the GPU core on CPU), results reassembled == single process."""
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cwbl import abi, synth
+from cwbl import dist as cdist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _analyse_oracle(w, xyz, obs, hdxb):
+    from helpers import oracle
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, xyz, obs, hdxb).build()
+    var = w.var.copy()
+    st = abi.Stats()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(w.x, w.y, w.alt, var)), 1, C.byref(st))
+    assert rc == 0
+    return var, st.solved
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w = synth.make("c2", seed=5, scale=0.06, nz=6, rows=(rank, world))
+    n, k = w.obs.shape[0], w.k
+    buf = torch.zeros(cdist.packed_len(n, k), dtype=torch.float32)
+    if rank == 0:
+        buf.copy_(torch.from_numpy(cdist.pack_radar(w.obs_xyz, w.obs, w.hdxb)))
+    cdist.broadcast_obs(buf, src=0)
+    xyz, obs, hdxb = cdist.unpack_radar(buf.numpy(), n, k)
+    var, solved = _analyse_oracle(w, xyz, obs, hdxb)
+    np.save(os.path.join(out_dir, f"rank{rank}.npy"), var)
+    tot = torch.tensor([solved], dtype=torch.int64)
+    dist.all_reduce(tot)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "solved.npy"), tot.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_analysis_equals_single_process(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    full = synth.make("c2", seed=5, scale=0.06, nz=6)
+    ref, solved_ref = _analyse_oracle(full, full.obs_xyz, full.obs, full.hdxb)
+    got = np.empty_like(ref)
+    for r in range(world):
+        rows = cdist.shard_rows(full.var.shape[2], r, world)
+        got[:, :, rows, :] = np.load(tmp_path / f"rank{r}.npy")
+    np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert int(np.load(tmp_path / "solved.npy")[0]) == solved_ref
+
+
+def test_shard_rows_partition():
+    for ny in (1, 7, 300):
+        for world in (1, 2, 3, 8):
+            rows = np.concatenate([cdist.shard_rows(ny, r, world) for r in range(world)])
+            assert sorted(rows.tolist()) == list(range(ny))
+
+
+def test_pack_roundtrip():
+    rng = np.random.default_rng(0)
+    n, k = 17, 5
+    xyz, obs, hdxb = rng.random((n, 3)), rng.random(n), rng.random((k, n))
+    p = cdist.pack_radar(xyz, obs, hdxb)
+    assert p.shape[0] == cdist.packed_len(n, k)
+    a, b, c = cdist.unpack_radar(p, n, k)
+    np.testing.assert_array_equal(a, xyz.astype(np.float32))
+    np.testing.assert_array_equal(b, obs.astype(np.float32))
+    np.testing.assert_array_equal(c, hdxb.astype(np.float32))
