@@ -715,9 +715,17 @@ solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, lo
   __syncthreads();
   double wb = 0.0, sr = 0.0;  // wbar_r = (Pa Yb d)_r ; s_r = (Pa^{1/2} x')_r
 #pragma unroll
-  for (int q = 0; q < KP; ++q) {
-    wb = fma(v[q], sm.z1[q], wb);
-    sr = fma(v[q], sm.z2[q], sr);
+  for (int q = 0; q < KP; q += 4) {
+    // bounded groups: keeps the LDS loads of z1/z2 from all being hoisted at once
+    const double2 a0 = *reinterpret_cast<const double2 *>(&sm.z1[q]);
+    const double2 a1 = *reinterpret_cast<const double2 *>(&sm.z1[q + 2]);
+    const double2 b0 = *reinterpret_cast<const double2 *>(&sm.z2[q]);
+    const double2 b1 = *reinterpret_cast<const double2 *>(&sm.z2[q + 2]);
+    wb = fma(v[q], a0.x, wb); wb = fma(v[q + 1], a0.y, wb);
+    wb = fma(v[q + 2], a1.x, wb); wb = fma(v[q + 3], a1.y, wb);
+    sr = fma(v[q], b0.x, sr); sr = fma(v[q + 1], b0.y, sr);
+    sr = fma(v[q + 2], b1.x, sr); sr = fma(v[q + 3], b1.y, sr);
+    __builtin_amdgcn_sched_barrier(0);
   }
   const double xpl = lane < KP ? sm.xp[lane] : 0.0;
   const double d = wave_sum_f64(lane < k ? wb * xpl : 0.0);  // sum_i wbar_i x'_i

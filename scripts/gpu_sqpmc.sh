@@ -1,0 +1,23 @@
+#!/bin/bash
+# SQ PMC passes (issue/wait breakdown, LDS) on one bench step; kernel filter on the solve kernel
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/sq_${TAG:-r1}
+mkdir -p $OUT
+if [ -n "$WITH_TESTS" ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q -rf -x > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log; tail -3 gpurun_out/pytest_gpu.log
+  [ $rc -ne 0 ] && exit $rc
+fi
+timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > $OUT/bench.log 2>&1 || exit 4
+tail -1 $OUT/bench.log | cut -c1-400
+i=0
+for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
+         "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_INSTS_SMEM SQ_INSTS_BRANCH" \
+         "SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_FLAT SQ_LDS_UNALIGNED_STALL SQ_LDS_ADDR_CONFLICT SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64" ; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $P --kernel-include-regex solve_kernel -d $OUT/p$i -o p$i --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ${BENCH_ARGS} > $OUT/p$i.log 2>&1
+  rc=$?; echo "pass $i rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+done
+find $OUT -name "*.csv"
