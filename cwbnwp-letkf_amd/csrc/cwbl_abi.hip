@@ -91,6 +91,8 @@ struct State {
   DevBuf sx, sy, salt, svar;                          // slab staging (host-memory calls)
   DevBuf bcol, byo, byb, bxb, bxa, bev;               // solve_batch staging
   DevBuf qxyz, qnf, qidx, qr2;                        // search staging
+  DevBuf quad;                                        // x^-1/2 quadrature tables
+  bool jacobi = false;                                // CWBL_SOLVER=jacobi: eigen path
   std::vector<hipEvent_t> events;
 };
 
@@ -263,7 +265,7 @@ void release_all() {
   S.trees.clear();
   for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.nbr_r2, &S.info, &S.stats, &S.sx,
                     &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev,
-                    &S.qxyz, &S.qnf, &S.qidx, &S.qr2})
+                    &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad})
     b->release();
   for (hipEvent_t e : S.events) (void)hipEventDestroy(e);
   S.events.clear();
@@ -286,6 +288,7 @@ SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps,
   c.r2 = search_r2();
   c.max_sweeps = 30;
   if (const char *e = std::getenv("CWBL_DEBUG_MAX_SWEEPS")) c.max_sweeps = std::atoi(e);
+  c.quad = S.quad.as<double2>();
   return c;
 }
 
@@ -330,6 +333,14 @@ int cwbl_init(const cwbl_init_params *p) {
   S.q1_mode = p->q1_mode;
   S.ws_bytes = p->workspace_bytes ? p->workspace_bytes : (size_t(2) << 30);
   HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+  {
+    std::vector<double2> tab((size_t)kQuadLevels * 32);
+    for (int l = 1; l <= kQuadLevels; ++l) quad_table(l, &tab[(size_t)(l - 1) * 32]);
+    HIPCHK(S.quad.ensure(tab.size() * sizeof(double2)));
+    HIPCHK(hipMemcpy(S.quad.p, tab.data(), tab.size() * sizeof(double2), hipMemcpyHostToDevice));
+  }
+  const char *solver = std::getenv("CWBL_SOLVER");
+  S.jacobi = solver && std::strcmp(solver, "jacobi") == 0;
   S.inited = true;
   return CWBL_OK;
 }
@@ -496,9 +507,14 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     HIPCHK(launch_search(S.stream, dtrees, nt, list_cap, c.r2, sd, g0, nb,
                          S.nbr_cnt.as<int>(), S.nbr_idx.as<int>(), S.nbr_r2.as<float>(), dst));
     HIPCHK(hipEventRecord(b, S.stream));
-    HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, S.nbr_cnt.as<int>(),
-                                  S.nbr_idx.as<int>(), S.nbr_r2.as<float>(),
-                                  S.info.as<int2>()));
+    if (S.jacobi)
+      HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, S.nbr_cnt.as<int>(),
+                                    S.nbr_idx.as<int>(), S.nbr_r2.as<float>(),
+                                    S.info.as<int2>()));
+    else
+      HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, S.nbr_cnt.as<int>(),
+                             S.nbr_idx.as<int>(), S.nbr_r2.as<float>(), nullptr, nullptr,
+                             nullptr, nullptr, nullptr, S.info.as<int2>()));
     HIPCHK(hipEventRecord(cc, S.stream));
     HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), nb, dst));
     search_ev.push_back({ev, ev + 1});
@@ -564,8 +580,12 @@ int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const 
   }
   HIPCHK(S.info.ensure((size_t)npts * sizeof(int2)));
   SolveConsts c = solve_consts(inflat, use_rtpp, rtpp_alpha, use_rtps, rtps_alpha);
-  HIPCHK(launch_solve_assembled(S.stream, S.kp, c, npts, doff, dyo, dyb, dxb, dxa, dev,
-                                S.info.as<int2>()));
+  if (dev || S.jacobi)  // eigenvalues requested: the Jacobi eigensolver path
+    HIPCHK(launch_solve_assembled(S.stream, S.kp, c, npts, doff, dyo, dyb, dxb, dxa, dev,
+                                  S.info.as<int2>()));
+  else
+    HIPCHK(launch_solve_tq(S.stream, S.kp, true, nullptr, c, SlabDev{}, 0, npts, nullptr,
+                           nullptr, nullptr, doff, dyo, dyb, dxb, dxa, S.info.as<int2>()));
   if (memory != CWBL_MEM_DEVICE) {
     HIPCHK(hipMemcpyAsync(xa, dxa, (size_t)npts * k * 4, hipMemcpyDeviceToHost, S.stream));
     if (evals)

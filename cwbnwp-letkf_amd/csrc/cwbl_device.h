@@ -1,0 +1,281 @@
+// cwbl_device.h — device helpers shared by the HIP kernels of the LETKF core:
+// reference-exact fp32 weight functions, fp64 reciprocal helpers, cross-lane reductions,
+// and the column-assembly stage of the per-point solve (Yb Yb^T and Yb d in fp64).
+#pragma once
+
+#include "cwbl_internal.h"
+
+#include <hip/hip_runtime.h>
+
+namespace cwbl {
+
+// ---------------------------------------------------------------------------------------
+// fp32 helpers that must round exactly like the reference build
+// ---------------------------------------------------------------------------------------
+static __constant__ unsigned long long kExpT[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+
+// exp(real(4)) as the reference build evaluates it: glibc 2.35 expf, FMA variant
+// (table-driven, computed in double; the reference's flang `exp` calls libm expf).
+__device__ __forceinline__ float expf_ref(float x) {
+  const unsigned ux = __float_as_uint(x);
+  const unsigned abstop = (ux >> 20) & 0x7ffu;
+  if (abstop >= 0x42bu) {  // |x| >= 88: not reached on this path (0.25*r2 <= 3.34)
+    if (ux == 0xff800000u) return 0.0f;
+    return expf(x);
+  }
+  const double shift = __longlong_as_double(0x4338000000000000ll);
+  const double invln2n = __longlong_as_double(0x40471547652b82fell);
+  const double c0 = __longlong_as_double(0x3ebc6af84b912394ll);
+  const double c1 = __longlong_as_double(0x3f2ebfce50fac4f3ll);
+  const double c2 = __longlong_as_double(0x3f962e42ff0c52d6ll);
+  const double xd = (double)x;
+  double kd = fma(invln2n, xd, shift);
+  const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
+  kd = kd - shift;
+  const double r = fma(invln2n, xd, -kd);
+  unsigned long long t = kExpT[ki & 31ull];
+  t += ki << 47;
+  const double s = __longlong_as_double((long long)t);
+  const double z = fma(r, c0, c1);
+  const double r2 = r * r;
+  double y = fma(r, c2, 1.0);
+  y = fma(z, r2, y);
+  y = y * s;
+  return (float)y;
+}
+
+// Gaspari_Cohn_1999, module_localization.f90:333-364 (fp32, unfused)
+__device__ __forceinline__ float gaspari_cohn(float x) {
+  const float a = 1.82574189f;  // sqrt(10./3.) in fp32 (== sqrtf(10.0f/3.0f))
+  const float a1 = -0.25f, a2 = 0.5f, a3 = 0.625f, a4 = -5.0f / 3.0f, a5 = 1.0f;
+  const float b1 = 1.0f / 12.0f, b2 = -0.5f, b3 = 0.625f, b4 = 5.0f / 3.0f, b5 = -5.0f,
+              b6 = 4.0f, b7 = -2.0f / 3.0f;
+  const float z = x / a;
+  if (z <= 1.0f) return z * z * (z * (z * (a1 * z + a2) + a3) + a4) + a5;
+  if (z <= 2.0f) return z * (z * (z * (z * (b1 * z + b2) + b3) + b4) + b5) + b6 + b7 / z;
+  return 0.0f;
+}
+
+// localisation weight on the error, module_letkf_core.f90:443-450 / 516-523
+__device__ __forceinline__ float error_inv(int wf, float err, float r2) {
+  if (wf != 1) return 1.0f / (err * expf_ref(0.25f * r2));
+  return sqrtf(gaspari_cohn(sqrtf(r2))) / err;
+}
+
+
+// ---------------------------------------------------------------------------------------
+// fp64 helpers
+// ---------------------------------------------------------------------------------------
+// fp64 reciprocal / reciprocal square root: hardware estimate + two Newton steps (~1 ulp).
+// The rotation only needs c^2 + s^2 = 1 to working precision, not IEEE-rounded c and s.
+__device__ __forceinline__ double rcp64(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+__device__ __forceinline__ double rsq64(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double t = fma(-h * y, y, 0.5);
+  y = fma(y, t, y);
+  t = fma(-h * y, y, 0.5);
+  return fma(y, t, y);
+}
+
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  const int x = b & 7, l = b >> 3, q = n >> 3, r = n & 7;
+  return x * q + (x < r ? x : r) + l;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// DPP lane exchange of a double (two 32-bit moves).  Callers keep all 64 lanes active.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Sum over each 16-lane row; every lane of a row gets the same (bitwise) row sum.
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  return v;
+}
+
+// Wave-uniform sum over the 64 lanes (fixed order: rows 0+1, 2+3, then the two halves).
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  const double r = row16_sum(v);
+  return (readlane_f64(r, 0) + readlane_f64(r, 16)) + (readlane_f64(r, 32) + readlane_f64(r, 48));
+}
+
+// Sum over each half wave (lanes 0-31, 32-63); every lane gets its half's sum.
+__device__ __forceinline__ double half_sum_dpp(double v) {
+  const double r = row16_sum(v);
+  const double top = readlane_f64(r, 0) + readlane_f64(r, 16);
+  const double bot = readlane_f64(r, 32) + readlane_f64(r, 48);
+  return threadIdx.x < 32 ? top : bot;
+}
+
+// ---------------------------------------------------------------------------------------
+// Column assembly of one grid point (one wavefront): the point-dependent half of
+// letkf_yoyb (localisation weight on the error, module_letkf_core.f90:443-452) fused with
+// the Yb Yb^T (dsyrk) and Yb d products of letkf_solve (:598-700), in fp64.
+// Lane L owns the 4x4 blocks L, L+64, ... of the lower block triangle (bi >= bj).
+// ---------------------------------------------------------------------------------------
+template <int KP, int CHUNK>
+struct ColumnChunk {
+  float yb[CHUNK][KP];
+  float yo[CHUNK];
+  float w[CHUNK];
+  int col[CHUNK];
+};
+
+template <int KP>
+struct AsmLayout {
+  static constexpr int NB = KP / 4;                 // 4x4 blocks per dimension
+  static constexpr int NBLK = NB * (NB + 1) / 2;    // lower-triangle blocks
+  static constexpr int NBL = (NBLK + 63) / 64;      // blocks per lane
+};
+
+template <int KP, int CHUNK, bool ASSEMBLED>
+__device__ __forceinline__ void assemble_point(
+    ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
+    int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
+    const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
+    const float *__restrict__ yo_in, const float *__restrict__ yb_in,
+    const int (&bi)[AsmLayout<KP>::NBL], const int (&bj)[AsmLayout<KP>::NBL],
+    double (&acc)[AsmLayout<KP>::NBL][16], double &b1acc, int &ptot) {
+  constexpr int NBL = AsmLayout<KP>::NBL, NBLK = AsmLayout<KP>::NBLK;
+  const int k = c.k;
+#pragma unroll
+  for (int it = 0; it < NBL; ++it)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[it][e] = 0.0;
+  b1acc = 0.0;
+  ptot = 0;
+
+  // accumulate nsl staged columns into A (lower) and Yb d
+  auto accumulate = [&](int nsl) {
+    for (int s = 0; s < nsl; ++s) {
+#pragma unroll
+      for (int it = 0; it < NBL; ++it) {
+        if (lane + 64 * it < NBLK) {
+          const float4 ra = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bi[it]]);
+          const float4 rb = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bj[it]]);
+          const double a4[4] = {ra.x, ra.y, ra.z, ra.w};
+          const double b4[4] = {rb.x, rb.y, rb.z, rb.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[it][4 * r + q] = fma(a4[r], b4[q], acc[it][4 * r + q]);
+        }
+      }
+      if (lane < KP) b1acc = fma((double)ch.yb[s][lane], (double)ch.yo[s], b1acc);
+    }
+  };
+
+  if constexpr (!ASSEMBLED) {
+    for (int t = 0; t < c.ntrees; ++t) {
+      const TreeDesc &T = trees[t];
+      const int cnt = nbr_cnt[(long long)gi * c.ntrees + t];
+      const int nvar = T.nvar;
+      const int npairs = cnt * nvar;
+      const long long lbase = (long long)gi * c.list_cap + T.list_off;
+      for (int base = 0; base < npairs; base += CHUNK) {
+        const int q = base + lane;
+        bool ok = false;
+        int col = 0;
+        float w = 0.0f, yo = 0.0f;
+        if (lane < CHUNK && q < npairs) {
+          const int jn = q / nvar, v = q - jn * nvar;
+          col = nbr_idx[lbase + jn] * nvar + v;
+          ok = T.col_ok[col] != 0;
+          if (ok) {
+            w = error_inv(c.weight_function, T.col_err[col], nbr_r2[lbase + jn]);
+            yo = T.col_omm[col] * w;  // omm * error_inv (:451)
+          }
+        }
+        const unsigned long long mask = __ballot(ok);
+        const int nsl = __popcll(mask);
+        if (ok) {
+          const int slot = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+          ch.col[slot] = col;
+          ch.w[slot] = w;
+          ch.yo[slot] = yo;
+        }
+        __syncthreads();
+        if (nsl == 0) continue;
+        constexpr int V4 = KP / 4;
+        for (int e = lane; e < nsl * V4; e += 64) {
+          const int s = e / V4, c4 = e - s * V4;
+          const float4 g = reinterpret_cast<const float4 *>(T.col_bg + (long long)ch.col[s] * KP)[c4];
+          const float ws = ch.w[s];
+          float4 y;  // bg * error_inv (:452)
+          y.x = g.x * ws; y.y = g.y * ws; y.z = g.z * ws; y.w = g.w * ws;
+          *reinterpret_cast<float4 *>(&ch.yb[s][4 * c4]) = y;
+        }
+        __syncthreads();
+        accumulate(nsl);
+        ptot += nsl;
+        __syncthreads();
+      }
+    }
+  } else {
+    const long long c0 = col_off[gi], c1 = col_off[gi + 1];
+    const int ncol = (int)(c1 - c0);
+    for (int base = 0; base < ncol; base += CHUNK) {
+      const int nsl = min(CHUNK, ncol - base);
+      if (lane < nsl) ch.yo[lane] = yo_in[c0 + base + lane];
+      for (int e = lane; e < nsl * KP; e += 64) {
+        const int s = e / KP, m = e - s * KP;
+        ch.yb[s][m] = m < k ? yb_in[(c0 + base + s) * k + m] : 0.0f;
+      }
+      __syncthreads();
+      accumulate(nsl);
+      ptot += nsl;
+      __syncthreads();
+    }
+  }
+}
+
+// lane -> 4x4 block (bi, bj) of the lower block triangle, row-major over the triangle
+template <int KP>
+__device__ __forceinline__ void block_of_lane(int lane, int (&bi)[AsmLayout<KP>::NBL],
+                                              int (&bj)[AsmLayout<KP>::NBL]) {
+#pragma unroll
+  for (int it = 0; it < AsmLayout<KP>::NBL; ++it) {
+    const int b = lane + 64 * it;
+    int rr = 0;
+    while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;
+    bi[it] = rr;
+    bj[it] = b - rr * (rr + 1) / 2;
+  }
+}
+
+}  // namespace cwbl

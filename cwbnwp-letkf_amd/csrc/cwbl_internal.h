@@ -66,7 +66,14 @@ struct SolveConsts {
   float nmember_inv;          // 1.0/k (module_param.f90:245)
   float r2;                   // gc1999**2
   int   max_sweeps;           // Jacobi sweep cap (CWBL_DEBUG_MAX_SWEEPS overrides; ablation only)
+  const double2 *quad;        // [kQuadLevels][32] (t2, w) of the x^-1/2 rule (solve_tq_kernel)
 };
+
+// Inverse-square-root quadrature of solve_tq_kernel (quad_tables.cpp): level L = 1..12
+// covers spectra with max/min <= 10^L using kQuadNodes nodes (slot 31 of a level is unused).
+constexpr int kQuadNodes = 31;
+constexpr int kQuadLevels = 12;
+void quad_table(int level, double2 *out32);
 
 // Point enumeration of a slab: g = i + ix_lim*(j + iy_lim*kz).
 struct SlabDev {
@@ -101,6 +108,14 @@ hipError_t launch_solve_neighbors(hipStream_t s, int kp, const TreeDesc *trees,
 hipError_t launch_solve_assembled(hipStream_t s, int kp, SolveConsts c, int npts,
                                   const long long *col_off, const float *yo, const float *yb,
                                   const float *xb, float *xa, double *evals, int2 *info);
+
+// Tridiagonalisation + quadrature solve (cwbl_tq.hip); same data contract as the two
+// launchers above, no eigenvalue output.
+hipError_t launch_solve_tq(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,
+                           SolveConsts c, SlabDev slab, long long g0, int npts,
+                           const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                           const long long *col_off, const float *yo, const float *yb,
+                           const float *xb, float *xa, int2 *info);
 
 hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, float r2, int nq,
                                 const float *q_xyz, int max_lz, int *nfound, int *idx,

@@ -15,72 +15,11 @@
 // Built with -ffp-contract=off: every fp32 expression is evaluated unfused, in the
 // reference's order (amdflang x86-64 evaluates the Fortran that way; see oracle/).
 // fp64 code uses explicit fma() where a fused result is wanted.
-#include "cwbl_internal.h"
+#include "cwbl_device.h"
 
 #include <hip/hip_runtime.h>
 
 namespace cwbl {
-
-// ---------------------------------------------------------------------------------------
-// fp32 helpers that must round exactly like the reference build
-// ---------------------------------------------------------------------------------------
-__constant__ unsigned long long kExpT[32] = {
-    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
-    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
-    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
-    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
-    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
-    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
-    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
-    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
-
-// exp(real(4)) as the reference build evaluates it: glibc 2.35 expf, FMA variant
-// (table-driven, computed in double; the reference's flang `exp` calls libm expf).
-__device__ __forceinline__ float expf_ref(float x) {
-  const unsigned ux = __float_as_uint(x);
-  const unsigned abstop = (ux >> 20) & 0x7ffu;
-  if (abstop >= 0x42bu) {  // |x| >= 88: not reached on this path (0.25*r2 <= 3.34)
-    if (ux == 0xff800000u) return 0.0f;
-    return expf(x);
-  }
-  const double shift = __longlong_as_double(0x4338000000000000ll);
-  const double invln2n = __longlong_as_double(0x40471547652b82fell);
-  const double c0 = __longlong_as_double(0x3ebc6af84b912394ll);
-  const double c1 = __longlong_as_double(0x3f2ebfce50fac4f3ll);
-  const double c2 = __longlong_as_double(0x3f962e42ff0c52d6ll);
-  const double xd = (double)x;
-  double kd = fma(invln2n, xd, shift);
-  const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
-  kd = kd - shift;
-  const double r = fma(invln2n, xd, -kd);
-  unsigned long long t = kExpT[ki & 31ull];
-  t += ki << 47;
-  const double s = __longlong_as_double((long long)t);
-  const double z = fma(r, c0, c1);
-  const double r2 = r * r;
-  double y = fma(r, c2, 1.0);
-  y = fma(z, r2, y);
-  y = y * s;
-  return (float)y;
-}
-
-// Gaspari_Cohn_1999, module_localization.f90:333-364 (fp32, unfused)
-__device__ __forceinline__ float gaspari_cohn(float x) {
-  const float a = 1.82574189f;  // sqrt(10./3.) in fp32 (== sqrtf(10.0f/3.0f))
-  const float a1 = -0.25f, a2 = 0.5f, a3 = 0.625f, a4 = -5.0f / 3.0f, a5 = 1.0f;
-  const float b1 = 1.0f / 12.0f, b2 = -0.5f, b3 = 0.625f, b4 = 5.0f / 3.0f, b5 = -5.0f,
-              b6 = 4.0f, b7 = -2.0f / 3.0f;
-  const float z = x / a;
-  if (z <= 1.0f) return z * z * (z * (z * (a1 * z + a2) + a3) + a4) + a5;
-  if (z <= 2.0f) return z * (z * (z * (z * (b1 * z + b2) + b3) + b4) + b5) + b6 + b7 / z;
-  return 0.0f;
-}
-
-// localisation weight on the error, module_letkf_core.f90:443-450 / 516-523
-__device__ __forceinline__ float error_inv(int wf, float err, float r2) {
-  if (wf != 1) return 1.0f / (err * expf_ref(0.25f * r2));
-  return sqrtf(gaspari_cohn(sqrtf(r2))) / err;
-}
 
 // ---------------------------------------------------------------------------------------
 // obs_prep_kernel: one thread per column c = n*nvar + v of one obs type
@@ -333,35 +272,13 @@ struct Ring {
   }
 };
 
-// fp64 reciprocal / reciprocal square root: hardware estimate + two Newton steps (~1 ulp).
-// The rotation only needs c^2 + s^2 = 1 to working precision, not IEEE-rounded c and s.
-__device__ __forceinline__ double rcp64(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  double e = fma(-x, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-x, r, 1.0);
-  return fma(r, e, r);
-}
-__device__ __forceinline__ double rsq64(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  const double h = 0.5 * x;
-  double t = fma(-h * y, y, 0.5);
-  y = fma(y, t, y);
-  t = fma(-h * y, y, 0.5);
-  return fma(y, t, y);
-}
 
 template <int KP>
 struct SolveSmem {
   union {
     double A[KP + 1][KP + 2];  // work matrix (16-B aligned rows; last row = dummy
                                // target of padding writes) / eigenvectors at the end
-    struct {
-      float yb[kChunk][KP];
-      float yo[kChunk];
-      float w[kChunk];
-      int col[kChunk];
-    } ch;
+    ColumnChunk<KP, kChunk> ch;
   } u;
   double cs[KP / 2][2];  // c, s per pair
   double b1[KP];         // Yb d (fp64)
@@ -373,15 +290,7 @@ struct SolveSmem {
   float fscal[4];
 };
 
-__device__ __forceinline__ int xcd_remap(int b, int n) {
-  const int x = b & 7, l = b >> 3, q = n >> 3, r = n & 7;
-  return x * q + (x < r ? x : r) + l;
-}
 
-__device__ __forceinline__ double wave_sum_f64(double v) {
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
 
 template <int KP, bool ASSEMBLED>
 __global__ void __launch_bounds__(64)
@@ -392,9 +301,6 @@ solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, lo
              const float *__restrict__ xb_in, float *__restrict__ xa_out,
              double *__restrict__ evals, int2 *__restrict__ info) {
   static_assert(KP % 8 == 0 && KP <= 64, "KP");
-  constexpr int NB = KP / 4;                     // 4x4 blocks per dimension
-  constexpr int NBLK = NB * (NB + 1) / 2;        // lower-triangle blocks
-  constexpr int NBL = (NBLK + 63) / 64;          // blocks per lane
   constexpr int NP = KP / 2;                     // pairs per step
   constexpr int NPB = NP * (NP + 1) / 2;         // pair blocks (lower)
   constexpr int NPL = (NPB + 63) / 64;
@@ -418,107 +324,14 @@ solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, lo
     if (lane < KP) sm.xb[lane] = lane < k ? xb_in[(long long)gi * k + lane] : 0.0f;
   }
 
-  // ---- lane -> 4x4 block of the lower triangle of A --------------------------------
+  constexpr int NBL = AsmLayout<KP>::NBL, NBLK = AsmLayout<KP>::NBLK;
   int bi[NBL], bj[NBL];
-#pragma unroll
-  for (int it = 0; it < NBL; ++it) {
-    const int b = lane + 64 * it;
-    int rr = 0;
-    while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;
-    bi[it] = rr;
-    bj[it] = b - rr * (rr + 1) / 2;
-  }
+  block_of_lane<KP>(lane, bi, bj);
   double acc[NBL][16];
-#pragma unroll
-  for (int it = 0; it < NBL; ++it)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[it][e] = 0.0;
-  double b1acc = 0.0;
-  int ptot = 0;
-
-  // accumulate nsl staged columns into A (lower) and Yb d
-  auto accumulate = [&](int nsl) {
-    for (int s = 0; s < nsl; ++s) {
-#pragma unroll
-      for (int it = 0; it < NBL; ++it) {
-        if (lane + 64 * it < NBLK) {
-          const float4 ra = *reinterpret_cast<const float4 *>(&sm.u.ch.yb[s][4 * bi[it]]);
-          const float4 rb = *reinterpret_cast<const float4 *>(&sm.u.ch.yb[s][4 * bj[it]]);
-          const double a4[4] = {ra.x, ra.y, ra.z, ra.w};
-          const double b4[4] = {rb.x, rb.y, rb.z, rb.w};
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[it][4 * r + q] = fma(a4[r], b4[q], acc[it][4 * r + q]);
-        }
-      }
-      if (lane < KP) b1acc = fma((double)sm.u.ch.yb[s][lane], (double)sm.u.ch.yo[s], b1acc);
-    }
-  };
-
-  if constexpr (!ASSEMBLED) {
-    for (int t = 0; t < c.ntrees; ++t) {
-      const TreeDesc &T = trees[t];
-      const int cnt = nbr_cnt[(long long)gi * c.ntrees + t];
-      const int nvar = T.nvar;
-      const int npairs = cnt * nvar;
-      const long long lbase = (long long)gi * c.list_cap + T.list_off;
-      for (int base = 0; base < npairs; base += 64) {
-        const int q = base + lane;
-        bool ok = false;
-        int col = 0;
-        float w = 0.0f, yo = 0.0f;
-        if (q < npairs) {
-          const int jn = q / nvar, v = q - jn * nvar;
-          col = nbr_idx[lbase + jn] * nvar + v;
-          ok = T.col_ok[col] != 0;
-          if (ok) {
-            w = error_inv(c.weight_function, T.col_err[col], nbr_r2[lbase + jn]);
-            yo = T.col_omm[col] * w;  // omm * error_inv (:451)
-          }
-        }
-        const unsigned long long mask = __ballot(ok);
-        const int nsl = __popcll(mask);
-        if (ok) {
-          const int slot = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-          sm.u.ch.col[slot] = col;
-          sm.u.ch.w[slot] = w;
-          sm.u.ch.yo[slot] = yo;
-        }
-        __syncthreads();
-        if (nsl == 0) continue;
-        constexpr int V4 = KP / 4;
-        for (int e = lane; e < nsl * V4; e += 64) {
-          const int s = e / V4, c4 = e - s * V4;
-          const float4 g = reinterpret_cast<const float4 *>(T.col_bg + (long long)sm.u.ch.col[s] * KP)[c4];
-          const float ws = sm.u.ch.w[s];
-          float4 y;  // bg * error_inv (:452)
-          y.x = g.x * ws; y.y = g.y * ws; y.z = g.z * ws; y.w = g.w * ws;
-          *reinterpret_cast<float4 *>(&sm.u.ch.yb[s][4 * c4]) = y;
-        }
-        __syncthreads();
-        accumulate(nsl);
-        ptot += nsl;
-        __syncthreads();
-      }
-    }
-  } else {
-    const long long c0 = col_off[gi], c1 = col_off[gi + 1];
-    const int ncol = (int)(c1 - c0);
-    for (int base = 0; base < ncol; base += kChunk) {
-      const int nsl = min(kChunk, ncol - base);
-      if (lane < nsl) sm.u.ch.yo[lane] = yo_in[c0 + base + lane];
-      for (int e = lane; e < nsl * KP; e += 64) {
-        const int s = e / KP, m = e - s * KP;
-        sm.u.ch.yb[s][m] = m < k ? yb_in[(c0 + base + s) * k + m] : 0.0f;
-      }
-      __syncthreads();
-      accumulate(nsl);
-      ptot += nsl;
-      __syncthreads();
-    }
-  }
+  double b1acc;
+  int ptot;
+  assemble_point<KP, kChunk, ASSEMBLED>(sm.u.ch, trees, c, gi, lane, nbr_cnt, nbr_idx, nbr_r2,
+                                        col_off, yo_in, yb_in, bi, bj, acc, b1acc, ptot);
 
   if (ptot == 0) {  // no accepted observation: var left unchanged (:220, :226)
     if (lane == 0 && info) info[gi] = make_int2(0, 0);

@@ -57,6 +57,24 @@ def test_solve_batch_matches_reference(k):
     assert worst_eig <= EIG_TOL, worst_eig
 
 
+@pytest.mark.parametrize("k", [8, 40, 64])
+def test_solve_batch_tq_matches_reference(k):
+    """Without an eigenvalue output cwbl_solve_batch runs the tridiagonalisation + quadrature
+    kernel (cwbl_tq.hip): same increments as the reference's dsyevd path."""
+    g = golden(f"solve_k{k}.npz")
+    c = core(k)
+    col = g["col_off"]
+    worst = 0.0
+    for i in range(len(g["xb"])):
+        off = np.array([0, col[i + 1] - col[i]], np.int64)
+        xa, _ = c.solve_batch(off, g["yo"][col[i]:col[i + 1]], g["yb"][col[i] * k:col[i + 1] * k],
+                              g["xb"][i][None], inflat_of(k, g["multi_infl"][i]),
+                              int(g["use_rtpp"][i]), float(g["rtpp_alpha"][i]),
+                              int(g["use_rtps"][i]), float(g["rtps_alpha"][i]))
+        worst = max(worst, increment_rel_rms(xa[0], g["xa"][i], g["xb"][i]))
+    assert worst <= INCR_TOL, worst
+
+
 def test_k128_reports_unsupported():
     with pytest.raises(abi.CwblError, match="UNSUPPORTED"):
         abi.Core(128, device=0)
@@ -185,4 +203,23 @@ def test_c2_full_size_properties():
                                   16, C.byref(abi.Stats()))
     assert rc == 0
     rel = increment_rel_rms(sub(var), ref, sub(w.var))
+    assert rel <= INCR_TOL, rel
+
+
+@pytest.mark.parametrize("name", ["driver_mixed.npz", "driver_gc_k40.npz"])
+def test_tq_and_jacobi_solvers_agree(name, monkeypatch):
+    """The two solve kernels (eigendecomposition by Jacobi, CWBL_SOLVER=jacobi; and the
+    default tridiagonalisation + quadrature) give the same analysis to the tolerance."""
+    case = DriverCase(name)
+    out = {}
+    for solver in ("jacobi", "tq"):
+        monkeypatch.setenv("CWBL_SOLVER", solver)
+        _cores.clear()
+        c = abi.Core(case.k, device=0, weight_function=case.wf, norain_value=case.norain)
+        c.set_obs(case.obs_set())
+        slab, var = case.slab()
+        c.analyze_var(case.vp, slab)
+        c.finalize()
+        out[solver] = var
+    rel = increment_rel_rms(out["tq"], out["jacobi"], case.var_in)
     assert rel <= INCR_TOL, rel

@@ -1,0 +1,63 @@
+"""CPU tests of the inverse-square-root quadrature tables of the tridiagonal solve kernel
+(csrc/quad_tables.cpp, used by csrc/cwbl_tq.hip).  The tables are host code inside
+libcwbl.so; no GPU is needed.
+
+The rule: x^-1/2 ~= sum_j w_j / (t2_j + x) for x in [1, 10^L] (31 nodes, level L).  The
+kernel uses it on A/m with m = (k-1)/infl, whose spectrum lies in [1, trace(A)/m - (k-1)].
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from cwbl import abi
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return abi.load_library()
+
+
+def table(lib, level):
+    buf = np.zeros(64)
+    assert lib.cwbl_debug_quad_table(level, buf.ctypes.data_as(C.POINTER(C.c_double))) == 0
+    return buf.reshape(32, 2)[:31, 0], buf.reshape(32, 2)[:31, 1]
+
+
+# relative accuracy the kernel relies on, per decade of the spectrum
+BOUND = {1: 2e-15, 2: 2e-15, 3: 2e-15, 4: 2e-15, 5: 4e-15, 6: 2e-14, 7: 1e-13, 8: 5e-12}
+
+
+@pytest.mark.parametrize("level", sorted(BOUND))
+def test_rule_accuracy(lib, level):
+    t2, w = table(lib, level)
+    assert np.all(t2 > 0) and np.all(w > 0) and np.all(np.diff(t2) > 0)
+    lam = np.geomspace(1.0, 10.0 ** level, 20000)
+    approx = (w[None, :] / (t2[None, :] + lam[:, None])).sum(1)
+    err = np.max(np.abs(approx * np.sqrt(lam) - 1.0))
+    assert err <= BOUND[level], err
+
+
+def test_bad_level_rejected(lib):
+    buf = np.zeros(64)
+    p = buf.ctypes.data_as(C.POINTER(C.c_double))
+    assert lib.cwbl_debug_quad_table(0, p) != 0
+    assert lib.cwbl_debug_quad_table(13, p) != 0
+
+
+def test_matrix_function_on_spd_tridiagonal(lib):
+    """sum_j w_j (T + s_j I)^-1 u on a random SPD tridiagonal equals T^-1/2 u (eigh)."""
+    rng = np.random.default_rng(3)
+    n = 40
+    d = rng.uniform(30, 900, n)
+    e = rng.uniform(-100, 100, n - 1)
+    T = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+    lam, V = np.linalg.eigh(T)
+    assert lam[0] > 0
+    m = lam[0] * 0.9
+    level = int(np.ceil(np.log10(lam[-1] / m)))
+    t2, w = table(lib, level)
+    u = rng.normal(size=n)
+    y = sum(np.sqrt(m) * wj * np.linalg.solve(T + m * tj * np.eye(n), u) for tj, wj in zip(t2, w))
+    ref = V @ ((V.T @ u) / np.sqrt(lam))
+    assert np.max(np.abs(y - ref)) <= 1e-13 * np.max(np.abs(ref))
