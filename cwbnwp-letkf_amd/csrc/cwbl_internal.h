@@ -67,6 +67,8 @@ struct SolveConsts {
   float r2;                   // gc1999**2
   int   max_sweeps;           // Jacobi sweep cap (CWBL_DEBUG_MAX_SWEEPS overrides; ablation only)
   const double2 *quad;        // [kQuadLevels][32] (t2, w) of the x^-1/2 rule (solve_tq_kernel)
+  int   debug_stop;           // CWBL_DEBUG_TQ_STOP: 1 = after assembly, 2 = after
+                              // tridiagonalisation, 3 = after quadrature (timing ablation only)
 };
 
 // Inverse-square-root quadrature of solve_tq_kernel (quad_tables.cpp): level L = 1..12

@@ -34,20 +34,30 @@ constexpr int kTqChunk = 32;  // columns staged per round (LDS budget: ~11 KB pe
 
 template <int KP>
 struct TqSmem {
+  static constexpr int NB = KP / 4;
+  static constexpr int PLD = 4 * NB + 4;  // pb row pitch: 2*PLD = 8*odd dwords, so the 8 block
+                                          // rows of a half wave hit disjoint bank octets
   union {
     ColumnChunk<KP, kTqChunk> ch;
-    double ah[KP / 2][KP + 2];        // half of A on its way into row registers
-    double hv[KP * (KP - 1) / 2];     // Householder vectors, packed (v_j has k-1-j entries)
+    struct {
+      double hv[KP * (KP - 1) / 2];       // Householder vectors, packed (v_j: k-1-j entries)
+      union {
+        double pb[NB][PLD];               // A v partials: pb[R][4c+r] = block (R,c), row r
+        // T and the transformed vectors, twice: [0] in row order, [1] mirrored (row KP-1-t),
+        // so that the top and bottom lanes of a twisted solve read at the same offsets
+        struct {
+          double md[2][KP];               // diagonal
+          double mc[2][KP];               // coupling to the previous (mirrored) row
+          double mu1[2][KP], mu2[2][KP];  // Q^T b1, Q^T x'
+        } t;
+      } x;
+    } h;
   } u;
-  double row[KP];                     // pivot row of the current step
-  double vb[KP], wb[KP];              // v and w of the current step (zero above the pivot)
-  // T and the transformed vectors, twice: [0] in row order, [1] mirrored (row KP-1-t), so
-  // that the top and bottom lanes of a twisted solve read them at the same offsets
-  double md[2][KP];                   // diagonal
-  double mc[2][KP];                   // coupling to the previous (mirrored) row
-  double mu1[2][KP], mu2[2][KP];      // Q^T b1, Q^T x'
-  double y[KP];                       // T^-1/2 u2
-  double tau[KP];                     // Householder scalars
+  double col[KP];                         // pivot column of the current step
+  double vb[KP], wb[KP];                  // v and w of the current step (zero above the pivot)
+  double td[KP], te[KP];                  // T: diagonal, sub-diagonal (te[i] couples i, i+1)
+  double y[KP];                           // T^-1/2 u2
+  double tau[KP];                         // Householder scalars
   float xb[KP], xa[KP];
   double scal[4];
   float fscal[4];
@@ -101,47 +111,30 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     return;
   }
 
-  // ---- A = inflat*I + Yb Yb^T into registers: lane i < KP holds row i -------------------
+  if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the rest
+    if (lane == 0 && info) info[gi] = make_int2(ptot, (int)(acc[0][0] + b1acc));
+    return;
+  }
+  // ---- A = inflat*I + Yb Yb^T, kept in the assembly's 4x4 register blocks ---------------
   const double inflat_r8 = (double)c.inflat;
-  double a[KP];
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int it = 0; it < NBL; ++it) {
+    if (lane + 64 * it < NBLK && bi[it] == bj[it]) {
 #pragma unroll
-    for (int it = 0; it < NBL; ++it) {
-      if (lane + 64 * it < NBLK) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int ii = 4 * bi[it] + r, jj = 4 * bj[it] + q;
-            double v = acc[it][4 * r + q];
-            if (ii == jj) v = ii < k ? v + inflat_r8 : 1.0;
-            if (ii / H == half) sm.u.ah[ii - half * H][jj] = v;
-            if (jj / H == half) sm.u.ah[jj - half * H][ii] = v;
-          }
+      for (int r = 0; r < 4; ++r) {
+        const int ii = 4 * bi[it] + r;
+        acc[it][5 * r] = ii < k ? acc[it][5 * r] + inflat_r8 : 1.0;
       }
     }
-    __syncthreads();
-    if (lane < KP && lane / H == half) {
-#pragma unroll
-      for (int q = 0; q < KP; q += 2) {
-        const double2 t = *reinterpret_cast<const double2 *>(&sm.u.ah[lane - half * H][q]);
-        a[q] = t.x;
-        a[q + 1] = t.y;
-      }
-    }
-    __syncthreads();
   }
   if (lane == 0) {  // xb_mean = sum(xb) * nmember_inv in fp32 (:671)
     float s = 0.0f;
-    for (int m = 0; m < k; ++m) s = s + sm.xb[m];
+    for (int mm = 0; mm < k; ++mm) s = s + sm.xb[mm];
     sm.scal[0] = (double)(s * c.nmember_inv);
   }
   if (lane < KP) {  // padding of T: decoupled unit rows
-    sm.md[0][lane] = 1.0;
-    sm.md[1][KP - 1 - lane] = 1.0;
-    sm.mc[0][lane] = 0.0;
-    sm.mc[1][lane] = 0.0;
+    sm.td[lane] = 1.0;
+    sm.te[lane] = 0.0;
     sm.tau[lane] = 0.0;
   }
   __syncthreads();
@@ -150,30 +143,35 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   double ub = (lane < KP) ? b1acc : 0.0;                          // Yb d, becomes Q^T b1
 
   // ---- Householder tridiagonalisation (lower, dsytd2 order) ------------------------------
+  // Lane L keeps its lower 4x4 blocks (bi, bj) of A.  Per step j: the blocks of block
+  // column j/4 publish column j; lane i < KP forms v_i; every block adds its row and
+  // (transposed) column partial of A v into pb; lane i sums row i of pb; A -= v w^T + w v^T
+  // block by block.
   double trace = 0.0;
   for (int j = 0; j < k; ++j) {
-    if (lane == j) {
+    const int J = j >> 2, qj = j & 3;
 #pragma unroll
-      for (int q = 0; q < KP; q += 2)
-        *reinterpret_cast<double2 *>(&sm.row[q]) = make_double2(a[q], a[q + 1]);
+    for (int it = 0; it < NBL; ++it) {
+      if (lane + 64 * it < NBLK && bj[it] == J) {
+        double cv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          cv[r] = qj == 0 ? acc[it][4 * r] : qj == 1 ? acc[it][4 * r + 1]
+                : qj == 2 ? acc[it][4 * r + 2] : acc[it][4 * r + 3];
+        *reinterpret_cast<double2 *>(&sm.col[4 * bi[it]]) = make_double2(cv[0], cv[1]);
+        *reinterpret_cast<double2 *>(&sm.col[4 * bi[it] + 2]) = make_double2(cv[2], cv[3]);
+      }
     }
     __syncthreads();
-    const double dj = sm.row[j];
+    const double dj = sm.col[j];
     trace += dj;
-    if (lane == 0) {
-      sm.md[0][j] = dj;
-      sm.md[1][KP - 1 - j] = dj;
-    }
+    if (lane == 0) sm.td[j] = dj;
     if (j >= k - 2) {  // trailing 2x2 block: already tridiagonal
-      if (j == k - 2 && lane == 0) {
-        const double ej = sm.row[j + 1];
-        sm.mc[0][j + 1] = ej;
-        sm.mc[1][KP - 1 - j] = ej;
-      }
+      if (j == k - 2 && lane == 0) sm.te[j] = sm.col[j + 1];
       continue;
     }
-    const double x = (lane > j + 1 && lane < k) ? sm.row[lane] : 0.0;
-    const double alpha = sm.row[j + 1];
+    const double x = (lane > j + 1 && lane < k) ? sm.col[lane] : 0.0;
+    const double alpha = sm.col[j + 1];
     const double xn2 = wave_sum_dpp(x * x);
     double tau = 0.0, beta = alpha, scal = 0.0;
     if (xn2 > 0.0) {  // dlarfg
@@ -182,25 +180,57 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
       scal = 1.0 / (alpha - beta);
     }
     if (lane == 0) {
-      sm.mc[0][j + 1] = beta;
-      sm.mc[1][KP - 1 - j] = beta;
+      sm.te[j] = beta;
       sm.tau[j] = tau;
     }
     if (tau == 0.0) continue;  // H_j = I (uniform)
     const double v = lane == j + 1 ? 1.0 : x * scal;
     const int off = j * (k - 1) - j * (j - 1) / 2;  // packed start of v_j
     if (lane < KP) sm.vb[lane] = v;
-    if (lane > j && lane < k) sm.u.hv[off + lane - (j + 1)] = v;
+    if (lane > j && lane < k) sm.u.h.hv[off + lane - (j + 1)] = v;
     __syncthreads();
-    // p = tau * A v (rows > j)
-    double p0 = 0.0, p1 = 0.0;
+    // partials of A v
+    double vi[NBL][4], vj[NBL][4];
 #pragma unroll
-    for (int q = 0; q < KP; q += 2) {
-      const double2 vv = *reinterpret_cast<const double2 *>(&sm.vb[q]);
-      p0 = fma(a[q], vv.x, p0);
-      p1 = fma(a[q + 1], vv.y, p1);
+    for (int it = 0; it < NBL; ++it) {
+      if (lane + 64 * it < NBLK) {
+        const double2 a0 = *reinterpret_cast<const double2 *>(&sm.vb[4 * bi[it]]);
+        const double2 a1 = *reinterpret_cast<const double2 *>(&sm.vb[4 * bi[it] + 2]);
+        const double2 b0 = *reinterpret_cast<const double2 *>(&sm.vb[4 * bj[it]]);
+        const double2 b1 = *reinterpret_cast<const double2 *>(&sm.vb[4 * bj[it] + 2]);
+        vi[it][0] = a0.x; vi[it][1] = a0.y; vi[it][2] = a1.x; vi[it][3] = a1.y;
+        vj[it][0] = b0.x; vj[it][1] = b0.y; vj[it][2] = b1.x; vj[it][3] = b1.y;
+        double pr[4], pc[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pr[r] = acc[it][4 * r] * vj[it][0];
+#pragma unroll
+          for (int q = 1; q < 4; ++q) pr[r] = fma(acc[it][4 * r + q], vj[it][q], pr[r]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pc[q] = acc[it][q] * vi[it][0];
+#pragma unroll
+          for (int r = 1; r < 4; ++r) pc[q] = fma(acc[it][4 * r + q], vi[it][r], pc[q]);
+        }
+        double *dst = &sm.u.h.x.pb[bi[it]][4 * bj[it]];
+        *reinterpret_cast<double2 *>(dst) = make_double2(pr[0], pr[1]);
+        *reinterpret_cast<double2 *>(dst + 2) = make_double2(pr[2], pr[3]);
+        if (bi[it] != bj[it]) {
+          double *dt = &sm.u.h.x.pb[bj[it]][4 * bi[it]];
+          *reinterpret_cast<double2 *>(dt) = make_double2(pc[0], pc[1]);
+          *reinterpret_cast<double2 *>(dt + 2) = make_double2(pc[2], pc[3]);
+        }
+      }
     }
-    const double p = (lane > j && lane < k) ? tau * (p0 + p1) : 0.0;
+    __syncthreads();
+    double pp = 0.0;
+    if (lane < KP) {
+      const double *prow = &sm.u.h.x.pb[lane >> 2][lane & 3];
+#pragma unroll
+      for (int cb = 0; cb < TqSmem<KP>::NB; ++cb) pp += prow[4 * cb];
+    }
+    const double p = (lane > j && lane < k) ? tau * pp : 0.0;
     const double s1 = wave_sum_dpp(p * v);
     const double s2 = wave_sum_dpp(v * ux);
     const double s3 = wave_sum_dpp(v * ub);
@@ -211,25 +241,47 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     __syncthreads();
     // A <- A - v w^T - w v^T (rows and columns <= j are untouched: v, w vanish there)
 #pragma unroll
-    for (int q = 0; q < KP; q += 2) {
-      const double2 vv = *reinterpret_cast<const double2 *>(&sm.vb[q]);
-      const double2 ww = *reinterpret_cast<const double2 *>(&sm.wb[q]);
-      a[q] = fma(-v, ww.x, fma(-w, vv.x, a[q]));
-      a[q + 1] = fma(-v, ww.y, fma(-w, vv.y, a[q + 1]));
+    for (int it = 0; it < NBL; ++it) {
+      if (lane + 64 * it < NBLK) {
+        const double2 a0 = *reinterpret_cast<const double2 *>(&sm.wb[4 * bi[it]]);
+        const double2 a1 = *reinterpret_cast<const double2 *>(&sm.wb[4 * bi[it] + 2]);
+        const double2 b0 = *reinterpret_cast<const double2 *>(&sm.wb[4 * bj[it]]);
+        const double2 b1 = *reinterpret_cast<const double2 *>(&sm.wb[4 * bj[it] + 2]);
+        const double wi[4] = {a0.x, a0.y, a1.x, a1.y};
+        const double wj[4] = {b0.x, b0.y, b1.x, b1.y};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            acc[it][4 * r + q] =
+                fma(-vi[it][r], wj[q], fma(-wi[r], vj[it][q], acc[it][4 * r + q]));
+      }
     }
   }
-  if (lane < KP) {
-    sm.mu1[0][lane] = ub;
-    sm.mu1[1][KP - 1 - lane] = ub;
-    sm.mu2[0][lane] = ux;
-    sm.mu2[1][KP - 1 - lane] = ux;
+  __syncthreads();
+  if (lane < KP) {  // T and Q^T b1, Q^T x' in row order and mirrored
+    const double di = sm.td[lane];
+    const double cprev = lane >= 1 ? sm.te[lane - 1] : 0.0;  // couples lane-1, lane
+    const double cmir = sm.te[KP - 1 - lane];                // couples KP-1-lane, KP-lane
+    sm.u.h.x.t.md[0][lane] = di;
+    sm.u.h.x.t.md[1][KP - 1 - lane] = di;
+    sm.u.h.x.t.mc[0][lane] = cprev;
+    sm.u.h.x.t.mc[1][lane] = cmir;
+    sm.u.h.x.t.mu1[0][lane] = ub;
+    sm.u.h.x.t.mu1[1][KP - 1 - lane] = ub;
+    sm.u.h.x.t.mu2[0][lane] = ux;
+    sm.u.h.x.t.mu2[1][KP - 1 - lane] = ux;
   }
   __syncthreads();
 
+  if (c.debug_stop == 2) {
+    if (lane == 0 && info) info[gi] = make_int2(ptot, (int)(trace + ux + ub));
+    return;
+  }
   // ---- T^-1/2 u2 by quadrature, u1^T T^-1 u2 exactly --------------------------------------
   // spectrum of A within [m, M]: m = inflat (A - inflat I = Yb Yb^T >= 0), M = trace(A)
   const double m = inflat_r8;
-  const double ratio = trace / m;
+  const double ratio = trace / m - (double)(k - 1);  // lam_max <= trace - (k-1) m
   int level = 1;
   double dec = 10.0;
   while (level < kQuadLevels && dec < ratio) {
@@ -243,7 +295,8 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     sigma = m * tw.x;
     omega = sqrt(m) * tw.y;
   }
-  const double *dd = sm.md[side], *cc = sm.mc[side], *uu = sm.mu2[side], *u1 = sm.mu1[side];
+  const auto &tt = sm.u.h.x.t;
+  const double *dd = tt.md[side], *cc = tt.mc[side], *uu = tt.mu2[side], *u1 = tt.mu1[side];
   double rd[H], g[H];
   double dl = dd[0] + sigma;
   g[0] = uu[0];
@@ -257,7 +310,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     rd[t] = rcp64(dl);
   }
   // meeting rows H-1 (top) and H (bottom): 2x2 solve with the partner lane's pivot
-  const double cm = sm.mc[0][H];
+  const double cm = tt.mc[0][H];
   const double dlo = __shfl_xor(dl, 32, 64), go = __shfl_xor(g[H - 1], 32, 64);
   double xv = (g[H - 1] * dlo - cm * go) / fma(dl, dlo, -cm * cm);
   double dot = u1[H - 1] * xv;  // node 31: u1 . T^-1 u2
@@ -275,13 +328,17 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   const double d = readlane_f64(dot, 31) + readlane_f64(dot, 63);  // wbar . x'
   __syncthreads();
 
+  if (c.debug_stop == 3) {
+    if (lane == 0 && info) info[gi] = make_int2(ptot, (int)d);
+    return;
+  }
   // ---- back-transform: y <- Q y = H_0 H_1 ... H_{k-3} y -----------------------------------
   double yl = lane < KP ? sm.y[lane] : 0.0;
   for (int j = k - 3; j >= 0; --j) {
     const double tj = sm.tau[j];
     if (tj == 0.0) continue;
     const int off = j * (k - 1) - j * (j - 1) / 2;
-    const double vj = (lane > j && lane < k) ? sm.u.hv[off + lane - (j + 1)] : 0.0;
+    const double vj = (lane > j && lane < k) ? sm.u.h.hv[off + lane - (j + 1)] : 0.0;
     const double s = wave_sum_dpp(vj * yl);
     yl = fma(-tj * s, vj, yl);
   }
