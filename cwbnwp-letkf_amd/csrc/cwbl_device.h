@@ -106,8 +106,8 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double x) {
   const long long b = __double_as_longlong(x);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, true);
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
@@ -127,18 +127,29 @@ __device__ __forceinline__ double row16_sum(double v) {
   return v;
 }
 
-// Wave-uniform sum over the 64 lanes (fixed order: rows 0+1, 2+3, then the two halves).
+// x[lane] + x[lane ^ 16] (PERM = 16) or x[lane] + x[lane ^ 32] (PERM = 32) with gfx950's
+// v_permlane{16,32}_swap; both lanes of a pair add in the same order (bitwise equal sums).
+template <int PERM>
+__device__ __forceinline__ double swap_add_f64(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = (int)b, hi = (int)(b >> 32);
+  auto rl = PERM == 16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                       : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  auto rh = PERM == 16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                       : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const double a = __longlong_as_double(((long long)rh[0] << 32) | (unsigned)rl[0]);
+  const double c = __longlong_as_double(((long long)rh[1] << 32) | (unsigned)rl[1]);
+  return a + c;
+}
+
+// Sum over the 64 lanes, the same value in every lane.
 __device__ __forceinline__ double wave_sum_dpp(double v) {
-  const double r = row16_sum(v);
-  return (readlane_f64(r, 0) + readlane_f64(r, 16)) + (readlane_f64(r, 32) + readlane_f64(r, 48));
+  return swap_add_f64<32>(swap_add_f64<16>(row16_sum(v)));
 }
 
 // Sum over each half wave (lanes 0-31, 32-63); every lane gets its half's sum.
 __device__ __forceinline__ double half_sum_dpp(double v) {
-  const double r = row16_sum(v);
-  const double top = readlane_f64(r, 0) + readlane_f64(r, 16);
-  const double bot = readlane_f64(r, 32) + readlane_f64(r, 48);
-  return threadIdx.x < 32 ? top : bot;
+  return swap_add_f64<16>(row16_sum(v));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -162,43 +173,17 @@ struct AsmLayout {
   static constexpr int NBL = (NBLK + 63) / 64;      // blocks per lane
 };
 
-template <int KP, int CHUNK, bool ASSEMBLED>
-__device__ __forceinline__ void assemble_point(
+// Stages the point's accepted columns CHUNK at a time into `ch` (yb = bg * error_inv,
+// yo = omm * error_inv, in the reference's fp32 order) and calls accumulate(nsl) on each
+// staged chunk.  Returns the number of accepted columns (p).
+template <int KP, int CHUNK, bool ASSEMBLED, class Acc>
+__device__ __forceinline__ int stage_columns(
     ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
     const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
-    const float *__restrict__ yo_in, const float *__restrict__ yb_in,
-    const int (&bi)[AsmLayout<KP>::NBL], const int (&bj)[AsmLayout<KP>::NBL],
-    double (&acc)[AsmLayout<KP>::NBL][16], double &b1acc, int &ptot) {
-  constexpr int NBL = AsmLayout<KP>::NBL, NBLK = AsmLayout<KP>::NBLK;
+    const float *__restrict__ yo_in, const float *__restrict__ yb_in, Acc &&accumulate) {
   const int k = c.k;
-#pragma unroll
-  for (int it = 0; it < NBL; ++it)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[it][e] = 0.0;
-  b1acc = 0.0;
-  ptot = 0;
-
-  // accumulate nsl staged columns into A (lower) and Yb d
-  auto accumulate = [&](int nsl) {
-    for (int s = 0; s < nsl; ++s) {
-#pragma unroll
-      for (int it = 0; it < NBL; ++it) {
-        if (lane + 64 * it < NBLK) {
-          const float4 ra = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bi[it]]);
-          const float4 rb = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bj[it]]);
-          const double a4[4] = {ra.x, ra.y, ra.z, ra.w};
-          const double b4[4] = {rb.x, rb.y, rb.z, rb.w};
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[it][4 * r + q] = fma(a4[r], b4[q], acc[it][4 * r + q]);
-        }
-      }
-      if (lane < KP) b1acc = fma((double)ch.yb[s][lane], (double)ch.yo[s], b1acc);
-    }
-  };
-
+  int ptot = 0;
   if constexpr (!ASSEMBLED) {
     for (int t = 0; t < c.ntrees; ++t) {
       const TreeDesc &T = trees[t];
@@ -262,6 +247,102 @@ __device__ __forceinline__ void assemble_point(
       __syncthreads();
     }
   }
+  return ptot;
+}
+
+// Column assembly on the VALU: lane L accumulates the 4x4 blocks L, L+64, ... of the lower
+// block triangle of Yb Yb^T, and lanes < KP the entries of Yb d.
+template <int KP, int CHUNK, bool ASSEMBLED>
+__device__ __forceinline__ void assemble_point(
+    ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
+    int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
+    const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
+    const float *__restrict__ yo_in, const float *__restrict__ yb_in,
+    const int (&bi)[AsmLayout<KP>::NBL], const int (&bj)[AsmLayout<KP>::NBL],
+    double (&acc)[AsmLayout<KP>::NBL][16], double &b1acc, int &ptot) {
+  constexpr int NBL = AsmLayout<KP>::NBL, NBLK = AsmLayout<KP>::NBLK;
+#pragma unroll
+  for (int it = 0; it < NBL; ++it)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[it][e] = 0.0;
+  b1acc = 0.0;
+  ptot = stage_columns<KP, CHUNK, ASSEMBLED>(
+      ch, trees, c, gi, lane, nbr_cnt, nbr_idx, nbr_r2, col_off, yo_in, yb_in, [&](int nsl) {
+        for (int s = 0; s < nsl; ++s) {
+#pragma unroll
+          for (int it = 0; it < NBL; ++it) {
+            if (lane + 64 * it < NBLK) {
+              const float4 ra = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bi[it]]);
+              const float4 rb = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bj[it]]);
+              const double a4[4] = {ra.x, ra.y, ra.z, ra.w};
+              const double b4[4] = {rb.x, rb.y, rb.z, rb.w};
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                  acc[it][4 * r + q] = fma(a4[r], b4[q], acc[it][4 * r + q]);
+            }
+          }
+          if (lane < KP) b1acc = fma((double)ch.yb[s][lane], (double)ch.yo[s], b1acc);
+        }
+      });
+}
+
+// Column assembly on the matrix cores (v_mfma_f64_16x16x4_f64): Y' = [Yb; yo] padded to
+// 16*NT rows, and the lower tiles (I >= J) of Y' Y'^T accumulate in registers
+// (C/D map: col = lane&15, row = (lane>>4) + 4*reg).  Row KP of Y' is yo when it fits in
+// the padding (YO_ROW), so row KP of the product is Yb d; otherwise Yb d is summed on the
+// VALU by lanes < KP.  Products of fp32 values are exact in fp64 and every tile is a
+// sequence of fp64 fused multiply-adds, like the dsyrk of the reference.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+template <int KP>
+struct MfmaLayout {
+  static constexpr int NT = (KP + 15) / 16;              // 16-row tiles per dimension
+  static constexpr bool YO_ROW = KP + 1 <= 16 * NT;      // yo rides in the padding
+  static constexpr int NTL = NT * (NT + 1) / 2;          // lower tiles
+};
+
+template <int KP, int CHUNK, bool ASSEMBLED>
+__device__ __forceinline__ void assemble_point_mfma(
+    ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
+    int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
+    const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
+    const float *__restrict__ yo_in, const float *__restrict__ yb_in,
+    f64x4 (&tile)[MfmaLayout<KP>::NTL], double &b1acc, int &ptot) {
+  using L = MfmaLayout<KP>;
+#pragma unroll
+  for (int t = 0; t < L::NTL; ++t) tile[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+  b1acc = 0.0;
+  const int kk = lane >> 4, m = lane & 15;
+  ptot = stage_columns<KP, CHUNK, ASSEMBLED>(
+      ch, trees, c, gi, lane, nbr_cnt, nbr_idx, nbr_r2, col_off, yo_in, yb_in, [&](int nsl) {
+        for (int s0 = 0; s0 < nsl; s0 += 4) {
+          const int s = s0 + kk;
+          const bool live = s < nsl;
+          double op[L::NT];
+#pragma unroll
+          for (int I = 0; I < L::NT; ++I) {
+            const int row = 16 * I + m;
+            float f = 0.0f;
+            if (live) {
+              if (row < KP) f = ch.yb[s][row];
+              else if (L::YO_ROW && row == KP) f = ch.yo[s];
+            }
+            op[I] = (double)f;
+          }
+          int t = 0;
+#pragma unroll
+          for (int I = 0; I < L::NT; ++I)
+#pragma unroll
+            for (int J = 0; J <= I; ++J, ++t)
+              tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[I], op[J], tile[t], 0, 0, 0);
+        }
+        if constexpr (!L::YO_ROW) {
+          for (int s = 0; s < nsl; ++s)
+            if (lane < KP) b1acc = fma((double)ch.yb[s][lane], (double)ch.yo[s], b1acc);
+        }
+      });
 }
 
 // lane -> 4x4 block (bi, bj) of the lower block triangle, row-major over the triangle

@@ -30,41 +30,55 @@
 
 namespace cwbl {
 
-constexpr int kTqChunk = 32;  // columns staged per round (LDS budget: ~11 KB per wave)
+constexpr int kTqChunk = 32;  // columns staged per round
 
+// LDS of one point (KP = 40: 9.8 KB, so 16 waves fit a CU).  The big union is reused by
+// phase: staged columns -> half of A -> {Householder vectors + A v partials}, then
+// {Householder vectors + Q^T b1, Q^T x', T^-1/2 u2}.  The A v partials of step j only need
+// block rows >= j/4 and sit at the top of the region, above the Householder vectors
+// written so far.
 template <int KP>
 struct TqSmem {
   static constexpr int NB = KP / 4;
   static constexpr int PLD = 4 * NB + 4;  // pb row pitch: 2*PLD = 8*odd dwords, so the 8 block
                                           // rows of a half wave hit disjoint bank octets
+  static constexpr int NHV = KP * (KP - 1) / 2;  // packed Householder vectors at k = KP
+  static constexpr int hv_off(int j) { return j * (KP - 1) - j * (j - 1) / 2; }
+  static constexpr int cap() {  // region size: vectors so far + partials of rows >= j/4
+    int m = NHV + KP;
+    for (int j = 0; j + 2 < KP; ++j) {
+      const int need = hv_off(j + 1) + (NB - j / 4) * PLD;
+      m = need > m ? need : m;
+    }
+    return m;
+  }
+  static constexpr int REG = cap();
+  static constexpr int pb_base(int J) { return REG - (NB - J) * PLD; }
   union {
     ColumnChunk<KP, kTqChunk> ch;
-    struct {
-      double hv[KP * (KP - 1) / 2];       // Householder vectors, packed (v_j: k-1-j entries)
-      union {
-        double pb[NB][PLD];               // A v partials: pb[R][4c+r] = block (R,c), row r
-        // T and the transformed vectors, twice: [0] in row order, [1] mirrored (row KP-1-t),
-        // so that the top and bottom lanes of a twisted solve read at the same offsets
-        struct {
-          double md[2][KP];               // diagonal
-          double mc[2][KP];               // coupling to the previous (mirrored) row
-          double mu1[2][KP], mu2[2][KP];  // Q^T b1, Q^T x'
-        } t;
-      } x;
-    } h;
+    double ah[KP / 2][KP + 2];            // half of A on its way from MFMA tiles to blocks
+    double reg[REG];                      // hv[0, NHV) | y after the loop | pb
   } u;
   double col[KP];                         // pivot column of the current step
-  double vb[KP], wb[KP];                  // v and w of the current step (zero above the pivot)
-  double td[KP], te[KP];                  // T: diagonal, sub-diagonal (te[i] couples i, i+1)
-  double y[KP];                           // T^-1/2 u2
+  double vb[KP];                          // v of the current step (zero above the pivot)
+  double wb[KP];                          // w of the current step; Yb d before the loop
+  // row i of T and the transformed vectors, one 32-B record per row so that a shifted solve
+  // reads a row with one address; record KP only holds c(KP-1,KP) = 0
+  double tq[KP + 1][4];                   // d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
   double tau[KP];                         // Householder scalars
   float xb[KP], xa[KP];
   double scal[4];
   float fscal[4];
 };
 
+// waves per SIMD the register allocation is held to (VGPR budget 512 / waves)
+template <int KP>
+struct TqOccupancy {
+  static constexpr int kWaves = KP <= 40 ? 4 : KP <= 48 ? 3 : 2;
+};
+
 template <int KP, bool ASSEMBLED>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, TqOccupancy<KP>::kWaves)
 solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, long long g0,
                 int npts, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
                 const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
@@ -74,7 +88,8 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   static_assert(KP % 8 == 0 && KP <= 64, "KP");
   constexpr int H = KP / 2;
   constexpr int NBL = AsmLayout<KP>::NBL, NBLK = AsmLayout<KP>::NBLK;
-  __shared__ TqSmem<KP> sm;
+  using SM = TqSmem<KP>;
+  __shared__ SM sm;
 
   const int gi = xcd_remap(blockIdx.x, gridDim.x);
   if (gi >= npts) return;
@@ -94,14 +109,12 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     if (lane < KP) sm.xb[lane] = lane < k ? xb_in[(long long)gi * k + lane] : 0.0f;
   }
 
-  int bi[NBL], bj[NBL];
-  block_of_lane<KP>(lane, bi, bj);
-  double acc[NBL][16];
+  f64x4 tile[MfmaLayout<KP>::NTL];
   double b1acc;
   int ptot;
-  assemble_point<KP, kTqChunk, ASSEMBLED>(sm.u.ch, trees, c, gi, lane, nbr_cnt, nbr_idx,
-                                          nbr_r2, col_off, yo_in, yb_in, bi, bj, acc, b1acc,
-                                          ptot);
+  assemble_point_mfma<KP, kTqChunk, ASSEMBLED>(sm.u.ch, trees, c, gi, lane, nbr_cnt, nbr_idx,
+                                               nbr_r2, col_off, yo_in, yb_in, tile, b1acc,
+                                               ptot);
 
   if (ptot == 0) {  // no accepted observation: var left unchanged (:220, :226)
     if (lane == 0 && info) info[gi] = make_int2(0, 0);
@@ -112,10 +125,49 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   }
 
   if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the rest
-    if (lane == 0 && info) info[gi] = make_int2(ptot, (int)(acc[0][0] + b1acc));
+    double t = b1acc;
+#pragma unroll
+    for (int q = 0; q < MfmaLayout<KP>::NTL; ++q) t += tile[q][0] + tile[q][3];
+    if (lane == 0 && info) info[gi] = make_int2(ptot, (int)t);
     return;
   }
-  // ---- A = inflat*I + Yb Yb^T, kept in the assembly's 4x4 register blocks ---------------
+  // ---- A = inflat*I + Yb Yb^T: MFMA tiles -> LDS (two row halves) -> 4x4 register blocks --
+  int bi[NBL], bj[NBL];
+  block_of_lane<KP>(lane, bi, bj);
+  double acc[NBL][16];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    int t = 0;
+#pragma unroll
+    for (int I = 0; I < MfmaLayout<KP>::NT; ++I)
+#pragma unroll
+      for (int J = 0; J <= I; ++J, ++t) {
+        const int col = 16 * J + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * I + (lane >> 4) + 4 * r;
+          if (row / H == half && row < KP && col < KP) sm.u.ah[row - half * H][col] = tile[t][r];
+          if (MfmaLayout<KP>::YO_ROW && half == 0 && row == KP && col < KP)
+            sm.wb[col] = tile[t][r];  // row KP of Y' Y'^T = Yb d
+        }
+      }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) {
+      if (lane + 64 * it < NBLK && (4 * bi[it]) / H == half) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double *src = &sm.u.ah[4 * bi[it] + r - half * H][4 * bj[it]];
+          const double2 x0 = *reinterpret_cast<const double2 *>(src);
+          const double2 x1 = *reinterpret_cast<const double2 *>(src + 2);
+          acc[it][4 * r] = x0.x; acc[it][4 * r + 1] = x0.y;
+          acc[it][4 * r + 2] = x1.x; acc[it][4 * r + 3] = x1.y;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (MfmaLayout<KP>::YO_ROW && lane < KP) b1acc = sm.wb[lane];
   const double inflat_r8 = (double)c.inflat;
 #pragma unroll
   for (int it = 0; it < NBL; ++it) {
@@ -133,10 +185,11 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     sm.scal[0] = (double)(s * c.nmember_inv);
   }
   if (lane < KP) {  // padding of T: decoupled unit rows
-    sm.td[lane] = 1.0;
-    sm.te[lane] = 0.0;
+    sm.tq[lane][0] = 1.0;
+    sm.tq[lane][1] = 0.0;
     sm.tau[lane] = 0.0;
   }
+  if (lane == 0) sm.tq[KP][1] = 0.0;
   __syncthreads();
   const double xb_mean = sm.scal[0];
   double ux = (lane < k) ? (double)sm.xb[lane] - xb_mean : 0.0;  // x', becomes Q^T x'
@@ -148,16 +201,23 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   // (transposed) column partial of A v into pb; lane i sums row i of pb; A -= v w^T + w v^T
   // block by block.
   double trace = 0.0;
+  auto ld4 = [](const double *p, double (&o)[4]) {
+    const double2 a0 = *reinterpret_cast<const double2 *>(p);
+    const double2 a1 = *reinterpret_cast<const double2 *>(p + 2);
+    o[0] = a0.x; o[1] = a0.y; o[2] = a1.x; o[3] = a1.y;
+  };
   for (int j = 0; j < k; ++j) {
     const int J = j >> 2, qj = j & 3;
 #pragma unroll
     for (int it = 0; it < NBL; ++it) {
-      if (lane + 64 * it < NBLK && bj[it] == J) {
+      if (lane + 64 * it < NBLK && bj[it] == J) {  // publish column j
         double cv[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          cv[r] = qj == 0 ? acc[it][4 * r] : qj == 1 ? acc[it][4 * r + 1]
-                : qj == 2 ? acc[it][4 * r + 2] : acc[it][4 * r + 3];
+        switch (qj) {
+          case 0: for (int r = 0; r < 4; ++r) cv[r] = acc[it][4 * r]; break;
+          case 1: for (int r = 0; r < 4; ++r) cv[r] = acc[it][4 * r + 1]; break;
+          case 2: for (int r = 0; r < 4; ++r) cv[r] = acc[it][4 * r + 2]; break;
+          default: for (int r = 0; r < 4; ++r) cv[r] = acc[it][4 * r + 3]; break;
+        }
         *reinterpret_cast<double2 *>(&sm.col[4 * bi[it]]) = make_double2(cv[0], cv[1]);
         *reinterpret_cast<double2 *>(&sm.col[4 * bi[it] + 2]) = make_double2(cv[2], cv[3]);
       }
@@ -165,112 +225,111 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     __syncthreads();
     const double dj = sm.col[j];
     trace += dj;
-    if (lane == 0) sm.td[j] = dj;
+    if (lane == 0) sm.tq[j][0] = dj;
     if (j >= k - 2) {  // trailing 2x2 block: already tridiagonal
-      if (j == k - 2 && lane == 0) sm.te[j] = sm.col[j + 1];
+      if (j == k - 2 && lane == 0) {
+        sm.tq[j + 1][1] = sm.col[j + 1];
+      }
       continue;
     }
     const double x = (lane > j + 1 && lane < k) ? sm.col[lane] : 0.0;
     const double alpha = sm.col[j + 1];
     const double xn2 = wave_sum_dpp(x * x);
     double tau = 0.0, beta = alpha, scal = 0.0;
-    if (xn2 > 0.0) {  // dlarfg
-      beta = -copysign(sqrt(fma(alpha, alpha, xn2)), alpha);
-      tau = (beta - alpha) / beta;
-      scal = 1.0 / (alpha - beta);
+    if (xn2 > 0.0) {  // dlarfg, with fp64 rcp/rsq refined to ~1 ulp
+      const double a2 = fma(alpha, alpha, xn2);
+      beta = -copysign(a2 * rsq64(a2), alpha);
+      tau = (beta - alpha) * rcp64(beta);
+      scal = rcp64(alpha - beta);
     }
     if (lane == 0) {
-      sm.te[j] = beta;
+      sm.tq[j + 1][1] = beta;
       sm.tau[j] = tau;
     }
     if (tau == 0.0) continue;  // H_j = I (uniform)
+    // v_i = x_i * scal (i > j+1), v_{j+1} = 1, 0 elsewhere
     const double v = lane == j + 1 ? 1.0 : x * scal;
-    const int off = j * (k - 1) - j * (j - 1) / 2;  // packed start of v_j
     if (lane < KP) sm.vb[lane] = v;
-    if (lane > j && lane < k) sm.u.h.hv[off + lane - (j + 1)] = v;
+    if (lane > j && lane < k) sm.u.reg[SM::hv_off(0) + j * (k - 1) - j * (j - 1) / 2 + lane - (j + 1)] = v;
+    const double s2 = wave_sum_dpp(v * ux);
+    const double s3 = wave_sum_dpp(v * ub);
+    ux = fma(-tau * s2, v, ux);
+    ub = fma(-tau * s3, v, ub);
     __syncthreads();
-    // partials of A v
-    double vi[NBL][4], vj[NBL][4];
+    // partials of A v (block rows >= J only: v vanishes above)
+    double *pb = &sm.u.reg[SM::pb_base(J)] - J * SM::PLD;  // pb[R * PLD + col], R >= J
+    double s1p = 0.0;  // this lane's share of v^T A v
 #pragma unroll
     for (int it = 0; it < NBL; ++it) {
-      if (lane + 64 * it < NBLK) {
-        const double2 a0 = *reinterpret_cast<const double2 *>(&sm.vb[4 * bi[it]]);
-        const double2 a1 = *reinterpret_cast<const double2 *>(&sm.vb[4 * bi[it] + 2]);
-        const double2 b0 = *reinterpret_cast<const double2 *>(&sm.vb[4 * bj[it]]);
-        const double2 b1 = *reinterpret_cast<const double2 *>(&sm.vb[4 * bj[it] + 2]);
-        vi[it][0] = a0.x; vi[it][1] = a0.y; vi[it][2] = a1.x; vi[it][3] = a1.y;
-        vj[it][0] = b0.x; vj[it][1] = b0.y; vj[it][2] = b1.x; vj[it][3] = b1.y;
+      if (lane + 64 * it < NBLK && bi[it] >= J) {
+        double vi[4], vj[4];
+        ld4(&sm.vb[4 * bi[it]], vi);
+        ld4(&sm.vb[4 * bj[it]], vj);
         double pr[4], pc[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          pr[r] = acc[it][4 * r] * vj[it][0];
+          pr[r] = acc[it][4 * r] * vj[0];
 #pragma unroll
-          for (int q = 1; q < 4; ++q) pr[r] = fma(acc[it][4 * r + q], vj[it][q], pr[r]);
+          for (int q = 1; q < 4; ++q) pr[r] = fma(acc[it][4 * r + q], vj[q], pr[r]);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          pc[q] = acc[it][q] * vi[it][0];
+          pc[q] = acc[it][q] * vi[0];
 #pragma unroll
-          for (int r = 1; r < 4; ++r) pc[q] = fma(acc[it][4 * r + q], vi[it][r], pc[q]);
+          for (int r = 1; r < 4; ++r) pc[q] = fma(acc[it][4 * r + q], vi[r], pc[q]);
         }
-        double *dst = &sm.u.h.x.pb[bi[it]][4 * bj[it]];
+        double sp = vi[0] * pr[0];
+#pragma unroll
+        for (int r = 1; r < 4; ++r) sp = fma(vi[r], pr[r], sp);
+        double *dst = pb + bi[it] * SM::PLD + 4 * bj[it];
         *reinterpret_cast<double2 *>(dst) = make_double2(pr[0], pr[1]);
         *reinterpret_cast<double2 *>(dst + 2) = make_double2(pr[2], pr[3]);
         if (bi[it] != bj[it]) {
-          double *dt = &sm.u.h.x.pb[bj[it]][4 * bi[it]];
-          *reinterpret_cast<double2 *>(dt) = make_double2(pc[0], pc[1]);
-          *reinterpret_cast<double2 *>(dt + 2) = make_double2(pc[2], pc[3]);
+          if (bj[it] >= J) {
+            double *dt = pb + bj[it] * SM::PLD + 4 * bi[it];
+            *reinterpret_cast<double2 *>(dt) = make_double2(pc[0], pc[1]);
+            *reinterpret_cast<double2 *>(dt + 2) = make_double2(pc[2], pc[3]);
+          }
+          sp = sp + sp;  // the transposed block contributes v_j^T B^T v_i = v_i^T B v_j
         }
+        s1p += sp;
       }
     }
+    const double s1 = tau * wave_sum_dpp(s1p);  // p . v with p = tau A v
     __syncthreads();
     double pp = 0.0;
-    if (lane < KP) {
-      const double *prow = &sm.u.h.x.pb[lane >> 2][lane & 3];
+    if (lane < KP && lane > j) {
+      const double *prow = pb + (lane >> 2) * SM::PLD + (lane & 3);
 #pragma unroll
-      for (int cb = 0; cb < TqSmem<KP>::NB; ++cb) pp += prow[4 * cb];
+      for (int cb = 0; cb < SM::NB; ++cb) pp += prow[4 * cb];
     }
     const double p = (lane > j && lane < k) ? tau * pp : 0.0;
-    const double s1 = wave_sum_dpp(p * v);
-    const double s2 = wave_sum_dpp(v * ux);
-    const double s3 = wave_sum_dpp(v * ub);
     const double w = fma(-0.5 * tau * s1, v, p);  // w = p - (tau/2)(p.v) v
-    ux = fma(-tau * s2, v, ux);
-    ub = fma(-tau * s3, v, ub);
     if (lane < KP) sm.wb[lane] = w;
     __syncthreads();
     // A <- A - v w^T - w v^T (rows and columns <= j are untouched: v, w vanish there)
 #pragma unroll
     for (int it = 0; it < NBL; ++it) {
-      if (lane + 64 * it < NBLK) {
-        const double2 a0 = *reinterpret_cast<const double2 *>(&sm.wb[4 * bi[it]]);
-        const double2 a1 = *reinterpret_cast<const double2 *>(&sm.wb[4 * bi[it] + 2]);
-        const double2 b0 = *reinterpret_cast<const double2 *>(&sm.wb[4 * bj[it]]);
-        const double2 b1 = *reinterpret_cast<const double2 *>(&sm.wb[4 * bj[it] + 2]);
-        const double wi[4] = {a0.x, a0.y, a1.x, a1.y};
-        const double wj[4] = {b0.x, b0.y, b1.x, b1.y};
+      if (lane + 64 * it < NBLK && bi[it] >= J) {
+        double vi[4], vj[4], wi[4], wj[4];
+        ld4(&sm.vb[4 * bi[it]], vi);
+        ld4(&sm.vb[4 * bj[it]], vj);
+        ld4(&sm.wb[4 * bi[it]], wi);
+        ld4(&sm.wb[4 * bj[it]], wj);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            acc[it][4 * r + q] =
-                fma(-vi[it][r], wj[q], fma(-wi[r], vj[it][q], acc[it][4 * r + q]));
+            acc[it][4 * r + q] = fma(-vi[r], wj[q], fma(-wi[r], vj[q], acc[it][4 * r + q]));
       }
     }
   }
-  __syncthreads();
-  if (lane < KP) {  // T and Q^T b1, Q^T x' in row order and mirrored
-    const double di = sm.td[lane];
-    const double cprev = lane >= 1 ? sm.te[lane - 1] : 0.0;  // couples lane-1, lane
-    const double cmir = sm.te[KP - 1 - lane];                // couples KP-1-lane, KP-lane
-    sm.u.h.x.t.md[0][lane] = di;
-    sm.u.h.x.t.md[1][KP - 1 - lane] = di;
-    sm.u.h.x.t.mc[0][lane] = cprev;
-    sm.u.h.x.t.mc[1][lane] = cmir;
-    sm.u.h.x.t.mu1[0][lane] = ub;
-    sm.u.h.x.t.mu1[1][KP - 1 - lane] = ub;
-    sm.u.h.x.t.mu2[0][lane] = ux;
-    sm.u.h.x.t.mu2[1][KP - 1 - lane] = ux;
+  // after the Householder vectors (the partials are dead): per side, in walk order, the
+  // quadrature sum (Ym) and node 31's exact solve (Zm)
+  double *Ym = &sm.u.reg[SM::NHV], *Zm = Ym + KP;
+  if (lane < KP) {
+    sm.tq[lane][2] = ub;
+    sm.tq[lane][3] = ux;
   }
   __syncthreads();
 
@@ -279,9 +338,10 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     return;
   }
   // ---- T^-1/2 u2 by quadrature, u1^T T^-1 u2 exactly --------------------------------------
-  // spectrum of A within [m, M]: m = inflat (A - inflat I = Yb Yb^T >= 0), M = trace(A)
+  // spectrum of A within [m, M]: m = inflat (A - inflat I = Yb Yb^T >= 0),
+  // M = trace(A) - (k-1) m (the other k-1 eigenvalues are >= m)
   const double m = inflat_r8;
-  const double ratio = trace / m - (double)(k - 1);  // lam_max <= trace - (k-1) m
+  const double ratio = trace / m - (double)(k - 1);
   int level = 1;
   double dec = 10.0;
   while (level < kQuadLevels && dec < ratio) {
@@ -295,50 +355,63 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     sigma = m * tw.x;
     omega = sqrt(m) * tw.y;
   }
-  const auto &tt = sm.u.h.x.t;
-  const double *dd = tt.md[side], *cc = tt.mc[side], *uu = tt.mu2[side], *u1 = tt.mu1[side];
-  double rd[H], g[H];
-  double dl = dd[0] + sigma;
-  g[0] = uu[0];
-  rd[0] = rcp64(dl);
+  // lane side 0 walks rows 0, 1, .. H-1; side 1 walks rows KP-1, KP-2, .. H (mirrored).
+  // Forward elimination towards the middle keeps, per row, h_t = g_t / dl_t and
+  // m_t = c_{t+1} / dl_t, so that back substitution is x_t = h_t - m_t x_{t+1}.
+  const int dir = side ? -4 : 4;
+  const double *q = &sm.tq[side ? KP - 1 : 0][0];
+  const int cs = side ? 5 : 1;  // coupling with the previous mirrored row: c(i-1,i) / c(i,i+1)
+  double hh[H], mm[H];
+  double dl = q[0] + sigma;
+  double gt = q[3];
+  double rdl = rcp64(dl);
 #pragma unroll
   for (int t = 1; t < H; ++t) {
-    const double ct = cc[t];
-    const double l = ct * rd[t - 1];
-    dl = fma(-l, ct, dd[t] + sigma);
-    g[t] = fma(-l, g[t - 1], uu[t]);
-    rd[t] = rcp64(dl);
+    const double *qt = q + dir * t;
+    const double ct = qt[cs];
+    const double l = ct * rdl;
+    hh[t - 1] = gt * rdl;
+    mm[t - 1] = l;  // = c_t / dl_{t-1}
+    asm volatile("" : "+v"(hh[t - 1]));  // materialise now: g_{t-1} and 1/dl_{t-1} die here
+    dl = fma(-l, ct, qt[0] + sigma);
+    gt = fma(-l, gt, qt[3]);
+    rdl = rcp64(dl);
+    __builtin_amdgcn_sched_barrier(0);  // keep the recurrence in order: bounded live ranges
   }
   // meeting rows H-1 (top) and H (bottom): 2x2 solve with the partner lane's pivot
-  const double cm = tt.mc[0][H];
-  const double dlo = __shfl_xor(dl, 32, 64), go = __shfl_xor(g[H - 1], 32, 64);
-  double xv = (g[H - 1] * dlo - cm * go) / fma(dl, dlo, -cm * cm);
-  double dot = u1[H - 1] * xv;  // node 31: u1 . T^-1 u2
+  const double cm = sm.tq[H][1];
+  const double dlo = __shfl_xor(dl, 32, 64), go = __shfl_xor(gt, 32, 64);
+  double xv = (gt * dlo - cm * go) / fma(dl, dlo, -cm * cm);
+  double *ym = Ym + side * H, *zm = Zm + side * H;
   {
     const double ys = half_sum_dpp(omega * xv);
-    if (node == 0) sm.y[side ? H : H - 1] = ys;
+    if (node == 0) ym[H - 1] = ys;
+    if (node == 31) zm[H - 1] = xv;
   }
 #pragma unroll
   for (int t = H - 2; t >= 0; --t) {
-    xv = (g[t] - cc[t + 1] * xv) * rd[t];
-    dot = fma(u1[t], xv, dot);
+    xv = fma(-mm[t], xv, hh[t]);
     const double ys = half_sum_dpp(omega * xv);
-    if (node == 0) sm.y[side ? KP - 1 - t : t] = ys;
+    if (node == 0) ym[t] = ys;
+    if (node == 31) zm[t] = xv;
+    __builtin_amdgcn_sched_barrier(0);
   }
-  const double d = readlane_f64(dot, 31) + readlane_f64(dot, 63);  // wbar . x'
   __syncthreads();
+  const int wi = lane < H ? lane : H + (KP - 1 - lane);  // walk slot of row `lane`
+  const double zl = lane < KP ? Zm[wi] : 0.0;
+  double yl = lane < KP ? Ym[wi] : 0.0;
+  const double d = wave_sum_dpp(lane < KP ? sm.tq[lane][2] * zl : 0.0);  // u1 . T^-1 u2
 
   if (c.debug_stop == 3) {
     if (lane == 0 && info) info[gi] = make_int2(ptot, (int)d);
     return;
   }
   // ---- back-transform: y <- Q y = H_0 H_1 ... H_{k-3} y -----------------------------------
-  double yl = lane < KP ? sm.y[lane] : 0.0;
   for (int j = k - 3; j >= 0; --j) {
     const double tj = sm.tau[j];
     if (tj == 0.0) continue;
     const int off = j * (k - 1) - j * (j - 1) / 2;
-    const double vj = (lane > j && lane < k) ? sm.u.h.hv[off + lane - (j + 1)] : 0.0;
+    const double vj = (lane > j && lane < k) ? sm.u.reg[off + lane - (j + 1)] : 0.0;
     const double s = wave_sum_dpp(vj * yl);
     yl = fma(-tj * s, vj, yl);
   }
