@@ -87,7 +87,7 @@ struct State {
   std::vector<ObsType> obs;  // gts entries first (family 0), then radar (family 1)
   bool have_obs = false;
   std::vector<std::unique_ptr<TreeBufs>> trees;
-  DevBuf tdesc, nbr_cnt, nbr_idx, nbr_r2, info, stats;
+  DevBuf tdesc, nbr_cnt, nbr_idx, info, stats;
   DevBuf sx, sy, salt, svar;                          // slab staging (host-memory calls)
   DevBuf bcol, byo, byb, bxb, bxa, bev;               // solve_batch staging
   DevBuf qxyz, qnf, qidx, qr2;                        // search staging
@@ -223,7 +223,7 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
     HIPCHK(launch_obs_prep(S.stream, S.k, S.kp, family, ot.type_id, ot.nvar, n,
                            ot.obs.as<float>(), ot.error.as<float>(), ot.hdxb.as<float>(),
                            ot.qc.as<int>(), tp->err_muti, tp->err_rej, is_assim, S.norain,
-                           tb->col_bg.as<float>(), tb->col_omm.as<float>(),
+                           tb->ind.as<int>(), tb->col_bg.as<float>(), tb->col_omm.as<float>(),
                            tb->col_err.as<float>(), tb->col_ok.as<uint8_t>()));
     TreeDesc d{};
     d.nodes = tb->nodes.as<TreeNode>();
@@ -263,7 +263,7 @@ void release_all() {
     t->col_omm.release(); t->col_err.release(); t->col_ok.release();
   }
   S.trees.clear();
-  for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.nbr_r2, &S.info, &S.stats, &S.sx,
+  for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.info, &S.stats, &S.sx,
                     &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev,
                     &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad})
     b->release();
@@ -482,13 +482,12 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   HIPCHK(hipEventRecord(e2, S.stream));
 
   // ---- batches of {search, solve} ---------------------------------------------------------
-  const size_t per_pt = (size_t)list_cap * 8 + (size_t)nt * 4 + 8;
+  const size_t per_pt = (size_t)list_cap * 4 + (size_t)nt * 4 + 8;
   long long B = (long long)(S.ws_bytes / per_pt);
   B = std::max<long long>(std::min<long long>(B, npts), 256);
   B = std::min<long long>(B, 1 << 22);
   HIPCHK(S.nbr_cnt.ensure((size_t)B * nt * 4));
   HIPCHK(S.nbr_idx.ensure((size_t)B * std::max(list_cap, 1) * 4));
-  HIPCHK(S.nbr_r2.ensure((size_t)B * std::max(list_cap, 1) * 4));
   HIPCHK(S.info.ensure((size_t)B * sizeof(int2)));
   HIPCHK(S.stats.ensure(sizeof(DevStats)));
   HIPCHK(hipMemsetAsync(S.stats.p, 0, sizeof(DevStats), S.stream));
@@ -506,16 +505,15 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b)); HIPCHK(event(ev + 2, &cc));
     HIPCHK(hipEventRecord(a, S.stream));
     HIPCHK(launch_search(S.stream, dtrees, nt, list_cap, c.r2, sd, g0, nb,
-                         S.nbr_cnt.as<int>(), S.nbr_idx.as<int>(), S.nbr_r2.as<float>(), dst));
+                         S.nbr_cnt.as<int>(), S.nbr_idx.as<int>(), nullptr, dst));
     HIPCHK(hipEventRecord(b, S.stream));
     if (S.jacobi)
       HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, S.nbr_cnt.as<int>(),
-                                    S.nbr_idx.as<int>(), S.nbr_r2.as<float>(),
-                                    S.info.as<int2>()));
+                                    S.nbr_idx.as<int>(), S.info.as<int2>()));
     else
       HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, S.nbr_cnt.as<int>(),
-                             S.nbr_idx.as<int>(), S.nbr_r2.as<float>(), nullptr, nullptr,
-                             nullptr, nullptr, nullptr, S.info.as<int2>()));
+                             S.nbr_idx.as<int>(), nullptr, nullptr, nullptr, nullptr,
+                             nullptr, S.info.as<int2>()));
     HIPCHK(hipEventRecord(cc, S.stream));
     HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), nb, dst));
     search_ev.push_back({ev, ev + 1});
@@ -586,7 +584,7 @@ int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const 
                                   S.info.as<int2>()));
   else
     HIPCHK(launch_solve_tq(S.stream, S.kp, true, nullptr, c, SlabDev{}, 0, npts, nullptr,
-                           nullptr, nullptr, doff, dyo, dyb, dxb, dxa, S.info.as<int2>()));
+                           nullptr, doff, dyo, dyb, dxb, dxa, S.info.as<int2>()));
   if (memory != CWBL_MEM_DEVICE) {
     HIPCHK(hipMemcpyAsync(xa, dxa, (size_t)npts * k * 4, hipMemcpyDeviceToHost, S.stream));
     if (evals)

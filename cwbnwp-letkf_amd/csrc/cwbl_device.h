@@ -152,6 +152,35 @@ __device__ __forceinline__ double half_sum_dpp(double v) {
   return swap_add_f64<16>(row16_sum(v));
 }
 
+// Grid point g of a slab (the enumeration g = i + ix_lim*(j + iy_lim*kz) of the reference's
+// point loop, module_letkf_core.f90:209-213): projected x, y and altitude.
+__device__ __forceinline__ void slab_point(const SlabDev &s, long long g, float &x, float &y,
+                                           float &z) {
+  const int i = (int)(g % s.ix_lim);
+  const long long r = g / s.ix_lim;
+  const int j = (int)(r % s.iy_lim);
+  const int kz = (int)(r / s.iy_lim);
+  x = s.x[i + (long long)s.nx * j];
+  y = s.y[i + (long long)s.nx * j];
+  z = s.alt[i + (long long)s.alt_nx * (j + (long long)s.alt_ny * kz)];
+}
+
+// Squared normalised distance of tree slot `slot` from the normalised query (q0, q1, q2),
+// evaluated exactly as the search does (process_terminal_node_fixedball,
+// module_kdtree2.f90:1654-1707), so the solve reproduces the search's r2 bit for bit.
+__device__ __forceinline__ float slot_r2(const TreeDesc &T, int slot, float q0, float q1,
+                                         float q2) {
+  const float4 d = T.rdata[slot];
+  const float dx = d.x - q0, dy = d.y - q1;
+  float sd = dx * dx;
+  sd = sd + dy * dy;
+  if (T.tree_dim == 3) {
+    const float dz = d.z - q2;
+    sd = sd + dz * dz;
+  }
+  return sd;
+}
+
 // ---------------------------------------------------------------------------------------
 // Column assembly of one grid point (one wavefront): the point-dependent half of
 // letkf_yoyb (localisation weight on the error, module_letkf_core.f90:443-452) fused with
@@ -180,13 +209,16 @@ template <int KP, int CHUNK, bool ASSEMBLED, class Acc>
 __device__ __forceinline__ int stage_columns(
     ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
-    const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
+    const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in, Acc &&accumulate) {
   const int k = c.k;
   int ptot = 0;
   if constexpr (!ASSEMBLED) {
     for (int t = 0; t < c.ntrees; ++t) {
       const TreeDesc &T = trees[t];
+      // get_lz normalisation of the point (module_localization.f90:243-253), as the search
+      const float q0 = pt.x * T.hclr_inv, q1 = pt.y * T.hclr_inv;
+      const float q2 = T.query3d ? pt.z * T.vclr_inv : 0.0f;
       const int cnt = nbr_cnt[(long long)gi * c.ntrees + t];
       const int nvar = T.nvar;
       const int npairs = cnt * nvar;
@@ -198,21 +230,22 @@ __device__ __forceinline__ int stage_columns(
         float w = 0.0f, yo = 0.0f;
         if (lane < CHUNK && q < npairs) {
           const int jn = q / nvar, v = q - jn * nvar;
-          col = nbr_idx[lbase + jn] * nvar + v;
+          const int slot = nbr_idx[lbase + jn];
+          col = slot * nvar + v;
           ok = T.col_ok[col] != 0;
           if (ok) {
-            w = error_inv(c.weight_function, T.col_err[col], nbr_r2[lbase + jn]);
+            w = error_inv(c.weight_function, T.col_err[col], slot_r2(T, slot, q0, q1, q2));
             yo = T.col_omm[col] * w;  // omm * error_inv (:451)
           }
         }
         const unsigned long long mask = __ballot(ok);
         const int nsl = __popcll(mask);
         if (ok) {
-          const int slot = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-          ch.col[slot] = col;
-          ch.w[slot] = w;
-          ch.yo[slot] = yo;
+          const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+          ch.col[pos] = col;
+          ch.w[pos] = w;
+          ch.yo[pos] = yo;
         }
         __syncthreads();
         if (nsl == 0) continue;
@@ -256,7 +289,7 @@ template <int KP, int CHUNK, bool ASSEMBLED>
 __device__ __forceinline__ void assemble_point(
     ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
-    const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
+    const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in,
     const int (&bi)[AsmLayout<KP>::NBL], const int (&bj)[AsmLayout<KP>::NBL],
     double (&acc)[AsmLayout<KP>::NBL][16], double &b1acc, int &ptot) {
@@ -267,7 +300,7 @@ __device__ __forceinline__ void assemble_point(
     for (int e = 0; e < 16; ++e) acc[it][e] = 0.0;
   b1acc = 0.0;
   ptot = stage_columns<KP, CHUNK, ASSEMBLED>(
-      ch, trees, c, gi, lane, nbr_cnt, nbr_idx, nbr_r2, col_off, yo_in, yb_in, [&](int nsl) {
+      ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in, [&](int nsl) {
         for (int s = 0; s < nsl; ++s) {
 #pragma unroll
           for (int it = 0; it < NBL; ++it) {
@@ -307,7 +340,7 @@ template <int KP, int CHUNK, bool ASSEMBLED>
 __device__ __forceinline__ void assemble_point_mfma(
     ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
-    const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
+    const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in,
     f64x4 (&tile)[MfmaLayout<KP>::NTL], double &b1acc, int &ptot) {
   using L = MfmaLayout<KP>;
@@ -316,7 +349,7 @@ __device__ __forceinline__ void assemble_point_mfma(
   b1acc = 0.0;
   const int kk = lane >> 4, m = lane & 15;
   ptot = stage_columns<KP, CHUNK, ASSEMBLED>(
-      ch, trees, c, gi, lane, nbr_cnt, nbr_idx, nbr_r2, col_off, yo_in, yb_in, [&](int nsl) {
+      ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in, [&](int nsl) {
         for (int s0 = 0; s0 < nsl; s0 += 4) {
           const int s = s0 + kk;
           const bool live = s < nsl;

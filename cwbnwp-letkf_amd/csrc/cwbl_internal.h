@@ -40,7 +40,8 @@ struct TreeDesc {
   const TreeNode *nodes;
   const float4   *rdata;      // rearranged normalised coords (x,y,z,0)
   const int      *ind;
-  // column table of this type for the current variable (one column per (obs, obs-var))
+  // column table of this type for the current variable, one column per (tree slot,
+  // obs-var): column slot*nvar + v belongs to obs ind[slot]
   const float    *col_bg;     // [n*nvar][KP] fp32 bg = hdxb - mean, zero padded
   const float    *col_omm;    // [n*nvar] obs - mean
   const float    *col_err;    // [n*nvar] error * err_muti
@@ -95,17 +96,17 @@ struct DevStats {
 hipError_t launch_obs_prep(hipStream_t s, int k, int kp, int family, int type_id, int nvar,
                            int nobs, const float *obs, const float *error, const float *hdxb,
                            const int *qc, const float err_muti[5], const float err_rej[5],
-                           const int is_assim[5], float norain, float *col_bg,
-                           float *col_omm, float *col_err, uint8_t *col_ok);
+                           const int is_assim[5], float norain, const int *slot_obs,
+                           float *col_bg, float *col_omm, float *col_err, uint8_t *col_ok);
 
 hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int list_cap,
                          float r2, SlabDev slab, long long g0, int npts, int *nbr_cnt,
                          int *nbr_idx, float *nbr_r2, DevStats *stats);
 
+// nbr_idx holds tree slots (search with nbr_r2 = nullptr); the solve recomputes r2
 hipError_t launch_solve_neighbors(hipStream_t s, int kp, const TreeDesc *trees,
                                   SolveConsts c, SlabDev slab, long long g0, int npts,
-                                  const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
-                                  int2 *info);
+                                  const int *nbr_cnt, const int *nbr_idx, int2 *info);
 
 hipError_t launch_solve_assembled(hipStream_t s, int kp, SolveConsts c, int npts,
                                   const long long *col_off, const float *yo, const float *yb,
@@ -115,7 +116,7 @@ hipError_t launch_solve_assembled(hipStream_t s, int kp, SolveConsts c, int npts
 // launchers above, no eigenvalue output.
 hipError_t launch_solve_tq(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,
                            SolveConsts c, SlabDev slab, long long g0, int npts,
-                           const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                           const int *nbr_cnt, const int *nbr_idx,
                            const long long *col_off, const float *yo, const float *yb,
                            const float *xb, float *xa, int2 *info);
 

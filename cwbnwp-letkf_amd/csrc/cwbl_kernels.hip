@@ -33,14 +33,18 @@ __global__ void __launch_bounds__(256)
 obs_prep_kernel(int k, int kp, int family, int type_id, int nvar, int nobs,
                 const float *__restrict__ obs, const float *__restrict__ error,
                 const float *__restrict__ hdxb, const int *__restrict__ qc, PrepParams pp,
-                float norain, float *__restrict__ col_bg, float *__restrict__ col_omm,
-                float *__restrict__ col_err, uint8_t *__restrict__ col_ok) {
-  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+                float norain, const int *__restrict__ slot_obs, float *__restrict__ col_bg,
+                float *__restrict__ col_omm, float *__restrict__ col_err,
+                uint8_t *__restrict__ col_ok) {
+  // output column cs = slot*nvar + v (tree slot order); input column c = obs*nvar + v
+  const long long cs = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long ncol = (long long)nobs * nvar;
-  if (c >= ncol) return;
-  const int n = (int)(c / nvar), v = (int)(c - (long long)n * nvar);
+  if (cs >= ncol) return;
+  const int slot = (int)(cs / nvar), v = (int)(cs - (long long)slot * nvar);
+  const int n = slot_obs ? slot_obs[slot] : slot;
+  const long long c = (long long)n * nvar + v;
   const long long mstride = ncol;  // hdxb(nvar,nobs,0:k-1): member stride = nvar*nobs
-  float *bg = col_bg + c * kp;
+  float *bg = col_bg + cs * kp;
   bool ok;
   float omm = 0.0f, err = 0.0f;
   if (family == 0) {
@@ -79,16 +83,16 @@ obs_prep_kernel(int k, int kp, int family, int type_id, int nvar, int nobs,
     err = e;
   }
   for (int m = ok ? k : 0; m < kp; ++m) bg[m] = 0.0f;
-  col_omm[c] = omm;
-  col_err[c] = err;
-  col_ok[c] = ok ? 1 : 0;
+  col_omm[cs] = omm;
+  col_err[cs] = err;
+  col_ok[cs] = ok ? 1 : 0;
 }
 
 hipError_t launch_obs_prep(hipStream_t s, int k, int kp, int family, int type_id, int nvar,
                            int nobs, const float *obs, const float *error, const float *hdxb,
                            const int *qc, const float err_muti[5], const float err_rej[5],
-                           const int is_assim[5], float norain, float *col_bg,
-                           float *col_omm, float *col_err, uint8_t *col_ok) {
+                           const int is_assim[5], float norain, const int *slot_obs,
+                           float *col_bg, float *col_omm, float *col_err, uint8_t *col_ok) {
   PrepParams pp;
   for (int i = 0; i < 5; ++i) {
     pp.err_muti[i] = err_muti[i];
@@ -99,8 +103,8 @@ hipError_t launch_obs_prep(hipStream_t s, int k, int kp, int family, int type_id
   if (ncol == 0) return hipSuccess;
   const unsigned grid = (unsigned)((ncol + 255) / 256);
   hipLaunchKernelGGL(obs_prep_kernel, dim3(grid), dim3(256), 0, s, k, kp, family, type_id,
-                     nvar, nobs, obs, error, hdxb, qc, pp, norain, col_bg, col_omm, col_err,
-                     col_ok);
+                     nvar, nobs, obs, error, hdxb, qc, pp, norain, slot_obs, col_bg, col_omm,
+                     col_err, col_ok);
   return hipGetLastError();
 }
 
@@ -139,8 +143,12 @@ __device__ int search_tree(const TreeDesc &T, float q0, float q1, float q2, floa
         }
         if (sd <= r2) {
           if (count == T.max_lz) { overflow = true; return count; }
-          out_idx[count] = T.ind[i];
-          out_r2[count] = sd;
+          if (out_r2) {  // cwbl_search: original obs index and distance
+            out_idx[count] = T.ind[i];
+            out_r2[count] = sd;
+          } else {       // analysis: the tree slot (columns are stored in slot order)
+            out_idx[count] = i;
+          }
           ++count;
         }
       }
@@ -218,8 +226,8 @@ search_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, floa
     bool ovf = false;
     int cnt = 0;
     if (T.max_lz > 0)
-      cnt = search_tree(T, q0, q1, q2, r2, nbr_idx + base, nbr_r2 + base, stk + threadIdx.x,
-                        ovf);
+      cnt = search_tree(T, q0, q1, q2, r2, nbr_idx + base, nbr_r2 ? nbr_r2 + base : nullptr,
+                        stk + threadIdx.x, ovf);
     nbr_cnt[(long long)gi * ntrees + t] = cnt;
     trunc += ovf ? 1u : 0u;
   }
@@ -296,7 +304,7 @@ template <int KP, bool ASSEMBLED>
 __global__ void __launch_bounds__(64)
 solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, long long g0,
              int npts, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
-             const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
+             const long long *__restrict__ col_off,
              const float *__restrict__ yo_in, const float *__restrict__ yb_in,
              const float *__restrict__ xb_in, float *__restrict__ xa_out,
              double *__restrict__ evals, int2 *__restrict__ info) {
@@ -312,6 +320,7 @@ solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, lo
   const int k = c.k;
 
   long long P = 0;  // var index of member 0
+  float3 pt = make_float3(0.0f, 0.0f, 0.0f);  // the point's projected x, y and altitude
   if constexpr (!ASSEMBLED) {
     const long long g = g0 + gi;
     const int i = (int)(g % slab.ix_lim);
@@ -320,6 +329,7 @@ solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, lo
     const int kz = (int)(r / slab.iy_lim);
     P = i + (long long)slab.nx * (j + (long long)slab.ny * kz);
     if (lane < KP) sm.xb[lane] = lane < k ? slab.var[P + slab.L * lane] : 0.0f;
+    slab_point(slab, g, pt.x, pt.y, pt.z);
   } else {
     if (lane < KP) sm.xb[lane] = lane < k ? xb_in[(long long)gi * k + lane] : 0.0f;
   }
@@ -330,7 +340,7 @@ solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, lo
   double acc[NBL][16];
   double b1acc;
   int ptot;
-  assemble_point<KP, kChunk, ASSEMBLED>(sm.u.ch, trees, c, gi, lane, nbr_cnt, nbr_idx, nbr_r2,
+  assemble_point<KP, kChunk, ASSEMBLED>(sm.u.ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt,
                                         col_off, yo_in, yb_in, bi, bj, acc, b1acc, ptot);
 
   if (ptot == 0) {  // no accepted observation: var left unchanged (:220, :226)
@@ -600,15 +610,15 @@ solve_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, lo
 template <int KP>
 static hipError_t launch_solve_kp(hipStream_t s, bool assembled, const TreeDesc *trees,
                                   SolveConsts c, SlabDev slab, long long g0, int npts,
-                                  const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                                  const int *nbr_cnt, const int *nbr_idx,
                                   const long long *col_off, const float *yo, const float *yb,
                                   const float *xb, float *xa, double *evals, int2 *info) {
   if (assembled)
     hipLaunchKernelGGL((solve_kernel<KP, true>), dim3(npts), dim3(64), 0, s, trees, c, slab,
-                       g0, npts, nbr_cnt, nbr_idx, nbr_r2, col_off, yo, yb, xb, xa, evals, info);
+                       g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa, evals, info);
   else
     hipLaunchKernelGGL((solve_kernel<KP, false>), dim3(npts), dim3(64), 0, s, trees, c, slab,
-                       g0, npts, nbr_cnt, nbr_idx, nbr_r2, col_off, yo, yb, xb, xa, evals, info);
+                       g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa, evals, info);
   return hipGetLastError();
 }
 
@@ -622,14 +632,14 @@ int supported_kp(int k) {
 
 static hipError_t dispatch_solve(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,
                                  SolveConsts c, SlabDev slab, long long g0, int npts,
-                                 const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                                 const int *nbr_cnt, const int *nbr_idx,
                                  const long long *col_off, const float *yo, const float *yb,
                                  const float *xb, float *xa, double *evals, int2 *info) {
   if (npts <= 0) return hipSuccess;
 #define CWBL_KP_CASE(K)                                                                      \
   case K:                                                                                    \
     return launch_solve_kp<K>(s, assembled, trees, c, slab, g0, npts, nbr_cnt, nbr_idx,      \
-                              nbr_r2, col_off, yo, yb, xb, xa, evals, info);
+                              col_off, yo, yb, xb, xa, evals, info);
   switch (kp) {
     CWBL_KP_CASE(8)
     CWBL_KP_CASE(16)
@@ -647,17 +657,17 @@ static hipError_t dispatch_solve(hipStream_t s, int kp, bool assembled, const Tr
 
 hipError_t launch_solve_neighbors(hipStream_t s, int kp, const TreeDesc *trees,
                                   SolveConsts c, SlabDev slab, long long g0, int npts,
-                                  const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                                  const int *nbr_cnt, const int *nbr_idx,
                                   int2 *info) {
-  return dispatch_solve(s, kp, false, trees, c, slab, g0, npts, nbr_cnt, nbr_idx, nbr_r2,
-                        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, info);
+  return dispatch_solve(s, kp, false, trees, c, slab, g0, npts, nbr_cnt, nbr_idx, nullptr,
+                        nullptr, nullptr, nullptr, nullptr, nullptr, info);
 }
 
 hipError_t launch_solve_assembled(hipStream_t s, int kp, SolveConsts c, int npts,
                                   const long long *col_off, const float *yo, const float *yb,
                                   const float *xb, float *xa, double *evals, int2 *info) {
   SlabDev none{};
-  return dispatch_solve(s, kp, true, nullptr, c, none, 0, npts, nullptr, nullptr, nullptr,
+  return dispatch_solve(s, kp, true, nullptr, c, none, 0, npts, nullptr, nullptr,
                         col_off, yo, yb, xb, xa, evals, info);
 }
 

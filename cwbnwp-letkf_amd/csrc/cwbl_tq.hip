@@ -81,7 +81,7 @@ template <int KP, bool ASSEMBLED>
 __global__ void __launch_bounds__(64, TqOccupancy<KP>::kWaves)
 solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, long long g0,
                 int npts, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
-                const float *__restrict__ nbr_r2, const long long *__restrict__ col_off,
+                const long long *__restrict__ col_off,
                 const float *__restrict__ yo_in, const float *__restrict__ yb_in,
                 const float *__restrict__ xb_in, float *__restrict__ xa_out,
                 int2 *__restrict__ info) {
@@ -97,6 +97,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   const int k = c.k;
 
   long long P = 0;  // var index of member 0
+  float3 pt = make_float3(0.0f, 0.0f, 0.0f);  // the point's projected x, y and altitude
   if constexpr (!ASSEMBLED) {
     const long long g = g0 + gi;
     const int i = (int)(g % slab.ix_lim);
@@ -105,6 +106,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     const int kz = (int)(r / slab.iy_lim);
     P = i + (long long)slab.nx * (j + (long long)slab.ny * kz);
     if (lane < KP) sm.xb[lane] = lane < k ? slab.var[P + slab.L * lane] : 0.0f;
+    slab_point(slab, g, pt.x, pt.y, pt.z);
   } else {
     if (lane < KP) sm.xb[lane] = lane < k ? xb_in[(long long)gi * k + lane] : 0.0f;
   }
@@ -113,7 +115,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   double b1acc;
   int ptot;
   assemble_point_mfma<KP, kTqChunk, ASSEMBLED>(sm.u.ch, trees, c, gi, lane, nbr_cnt, nbr_idx,
-                                               nbr_r2, col_off, yo_in, yb_in, tile, b1acc,
+                                               pt, col_off, yo_in, yb_in, tile, b1acc,
                                                ptot);
 
   if (ptot == 0) {  // no accepted observation: var left unchanged (:220, :226)
@@ -468,28 +470,28 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
 template <int KP>
 static hipError_t launch_tq_kp(hipStream_t s, bool assembled, const TreeDesc *trees,
                                SolveConsts c, SlabDev slab, long long g0, int npts,
-                               const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                               const int *nbr_cnt, const int *nbr_idx,
                                const long long *col_off, const float *yo, const float *yb,
                                const float *xb, float *xa, int2 *info) {
   if (assembled)
     hipLaunchKernelGGL((solve_tq_kernel<KP, true>), dim3(npts), dim3(64), 0, s, trees, c, slab,
-                       g0, npts, nbr_cnt, nbr_idx, nbr_r2, col_off, yo, yb, xb, xa, info);
+                       g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa, info);
   else
     hipLaunchKernelGGL((solve_tq_kernel<KP, false>), dim3(npts), dim3(64), 0, s, trees, c,
-                       slab, g0, npts, nbr_cnt, nbr_idx, nbr_r2, col_off, yo, yb, xb, xa, info);
+                       slab, g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa, info);
   return hipGetLastError();
 }
 
 hipError_t launch_solve_tq(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,
                            SolveConsts c, SlabDev slab, long long g0, int npts,
-                           const int *nbr_cnt, const int *nbr_idx, const float *nbr_r2,
+                           const int *nbr_cnt, const int *nbr_idx,
                            const long long *col_off, const float *yo, const float *yb,
                            const float *xb, float *xa, int2 *info) {
   if (npts <= 0) return hipSuccess;
   if (c.quad == nullptr) return hipErrorInvalidValue;
 #define CWBL_TQ_CASE(K)                                                                      \
   case K:                                                                                    \
-    return launch_tq_kp<K>(s, assembled, trees, c, slab, g0, npts, nbr_cnt, nbr_idx, nbr_r2, \
+    return launch_tq_kp<K>(s, assembled, trees, c, slab, g0, npts, nbr_cnt, nbr_idx,         \
                            col_off, yo, yb, xb, xa, info);
   switch (kp) {
     CWBL_TQ_CASE(8)
