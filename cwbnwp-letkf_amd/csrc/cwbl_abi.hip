@@ -73,9 +73,19 @@ struct ObsType {
   DevBuf obs, error, hdxb, qc;
 };
 
+// One k-d tree of an obs type and its column tables.  The tree depends only on the obs
+// coordinates and the normalisation (hclr, vclr, dimension), so it is kept across
+// cwbl_analyze_var calls of one obs set; the column tables are rebuilt per call (they
+// depend on the variable's QC parameters).
 struct TreeBufs {
+  int entry = -1, dim = 0;
+  float hinv = 0.0f, vinv = 0.0f;
   DevBuf nodes, rdata, ind, col_bg, col_omm, col_err, col_ok;
   HostTree host;
+  void release() {
+    nodes.release(); rdata.release(); ind.release(); col_bg.release();
+    col_omm.release(); col_err.release(); col_ok.release();
+  }
 };
 
 struct State {
@@ -86,7 +96,7 @@ struct State {
   hipStream_t stream = nullptr;
   std::vector<ObsType> obs;  // gts entries first (family 0), then radar (family 1)
   bool have_obs = false;
-  std::vector<std::unique_ptr<TreeBufs>> trees;
+  std::vector<std::unique_ptr<TreeBufs>> tree_cache;  // trees of the current obs set
   DevBuf tdesc, nbr_cnt, nbr_idx, info, stats;
   DevBuf sx, sy, salt, svar;                          // slab staging (host-memory calls)
   DevBuf bcol, byo, byb, bxb, bxa, bev;               // solve_batch staging
@@ -186,32 +196,43 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
     int q1u = 0;
     if (dim3 && !own3d) { dim3 = false; q1u = 1; }
     const int n = ot.nobs;
-    std::vector<float> nx(3 * (size_t)n);
-    for (int j = 0; j < n; ++j) {
-      nx[3 * j + 0] = ot.xyz[3 * j + 0] * pd.hinv;
-      nx[3 * j + 1] = ot.xyz[3 * j + 1] * pd.hinv;
-      nx[3 * j + 2] = dim3 ? ot.xyz[3 * j + 2] * pd.vinv : -1.0f;
+    const int tdim = dim3 ? 3 : 2;
+    TreeBufs *tb = nullptr;
+    for (auto &t : S.tree_cache)
+      if (t->entry == pd.entry && t->dim == tdim && t->hinv == pd.hinv &&
+          (!dim3 || t->vinv == pd.vinv))
+        tb = t.get();
+    if (!tb) {  // build_tree (:35-167) for this normalisation
+      std::vector<float> nx(3 * (size_t)n);
+      for (int j = 0; j < n; ++j) {
+        nx[3 * j + 0] = ot.xyz[3 * j + 0] * pd.hinv;
+        nx[3 * j + 1] = ot.xyz[3 * j + 1] * pd.hinv;
+        nx[3 * j + 2] = dim3 ? ot.xyz[3 * j + 2] * pd.vinv : -1.0f;
+      }
+      auto nt = std::make_unique<TreeBufs>();
+      nt->entry = pd.entry; nt->dim = tdim; nt->hinv = pd.hinv; nt->vinv = pd.vinv;
+      build_kdtree(nx.data(), n, tdim, nt->host);
+      if (tree_depth(nt->host) >= kSearchStackDepth)
+        return fail(CWBL_ERR_UNSUPPORTED, "k-d tree too deep (%d obs)", n);
+      const HostTree &h = nt->host;
+      HIPCHK(nt->nodes.ensure(h.nodes.size() * sizeof(TreeNode)));
+      HIPCHK(nt->rdata.ensure(h.rdata.size() * sizeof(float)));
+      HIPCHK(nt->ind.ensure(h.ind.size() * sizeof(int) + 4));
+      HIPCHK(hipMemcpyAsync(nt->nodes.p, h.nodes.data(), h.nodes.size() * sizeof(TreeNode),
+                            hipMemcpyHostToDevice, S.stream));
+      HIPCHK(hipMemcpyAsync(nt->rdata.p, h.rdata.data(), h.rdata.size() * sizeof(float),
+                            hipMemcpyHostToDevice, S.stream));
+      if (!h.ind.empty())
+        HIPCHK(hipMemcpyAsync(nt->ind.p, h.ind.data(), h.ind.size() * sizeof(int),
+                              hipMemcpyHostToDevice, S.stream));
+      tb = nt.get();
+      S.tree_cache.push_back(std::move(nt));
     }
-    auto tb = std::make_unique<TreeBufs>();
-    build_kdtree(nx.data(), n, dim3 ? 3 : 2, tb->host);
-    if (tree_depth(tb->host) >= kSearchStackDepth)
-      return fail(CWBL_ERR_UNSUPPORTED, "k-d tree too deep (%d obs)", n);
-    const HostTree &h = tb->host;
     const size_t ncol = (size_t)n * ot.nvar;
-    HIPCHK(tb->nodes.ensure(h.nodes.size() * sizeof(TreeNode)));
-    HIPCHK(tb->rdata.ensure(h.rdata.size() * sizeof(float)));
-    HIPCHK(tb->ind.ensure(h.ind.size() * sizeof(int) + 4));
     HIPCHK(tb->col_bg.ensure(ncol * S.kp * sizeof(float)));
     HIPCHK(tb->col_omm.ensure(ncol * sizeof(float)));
     HIPCHK(tb->col_err.ensure(ncol * sizeof(float)));
     HIPCHK(tb->col_ok.ensure(ncol));
-    HIPCHK(hipMemcpyAsync(tb->nodes.p, h.nodes.data(), h.nodes.size() * sizeof(TreeNode),
-                          hipMemcpyHostToDevice, S.stream));
-    HIPCHK(hipMemcpyAsync(tb->rdata.p, h.rdata.data(), h.rdata.size() * sizeof(float),
-                          hipMemcpyHostToDevice, S.stream));
-    if (!h.ind.empty())
-      HIPCHK(hipMemcpyAsync(tb->ind.p, h.ind.data(), h.ind.size() * sizeof(int),
-                            hipMemcpyHostToDevice, S.stream));
     // point-independent QC columns (letkf_yoyb :429-437 / :497-510)
     const cwbl_type_params *tp = pd.tp;
     int is_assim[5] = {0, 0, 0, 0, 0};
@@ -243,12 +264,13 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
     d.q1_undef = q1u;
     list_cap += tp->max_lz_pts;
     descs.push_back(d);
-    S.trees.push_back(std::move(tb));
   }
   return CWBL_OK;
 }
 
 void release_obs() {
+  for (auto &t : S.tree_cache) t->release();
+  S.tree_cache.clear();
   for (auto &o : S.obs) {
     o.obs.release(); o.error.release(); o.hdxb.release(); o.qc.release();
   }
@@ -258,11 +280,6 @@ void release_obs() {
 
 void release_all() {
   release_obs();
-  for (auto &t : S.trees) {
-    t->nodes.release(); t->rdata.release(); t->ind.release(); t->col_bg.release();
-    t->col_omm.release(); t->col_err.release(); t->col_ok.release();
-  }
-  S.trees.clear();
   for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.info, &S.stats, &S.sx,
                     &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev,
                     &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad})
@@ -434,12 +451,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   hipEvent_t e0, e1;
   HIPCHK(event(0, &e0));
   HIPCHK(hipEventRecord(e0, S.stream));
-  // ---- trees + column tables ------------------------------------------------------------
-  for (auto &t : S.trees) {
-    t->nodes.release(); t->rdata.release(); t->ind.release(); t->col_bg.release();
-    t->col_omm.release(); t->col_err.release(); t->col_ok.release();
-  }
-  S.trees.clear();
+  // ---- trees (cached per obs set) + column tables ------------------------------------------
   std::vector<TreeDesc> descs;
   int list_cap = 0;
   if (int rc = build_family(0, vp, descs, list_cap)) return rc;

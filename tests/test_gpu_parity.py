@@ -223,3 +223,26 @@ def test_tq_and_jacobi_solvers_agree(name, monkeypatch):
         out[solver] = var
     rel = increment_rel_rms(out["tq"], out["jacobi"], case.var_in)
     assert rel <= INCR_TOL, rel
+
+
+def test_tree_cache_across_variables():
+    """Trees are cached per obs set and normalisation; column tables are rebuilt per
+    variable.  A call with other localisation/QC parameters in between must not change the
+    result of a repeated call (and a fresh state gives the same bits)."""
+    import copy
+    case = DriverCase("driver_mixed.npz")
+    c = core(case.k, case.wf, case.norain)
+    c.set_obs(case.obs_set())
+    slab, var1 = case.slab()
+    c.analyze_var(case.vp, slab)
+    other = copy.deepcopy(case.vp)
+    for tp in list(other.gts) + list(other.radar):
+        tp.hclr = tp.hclr * 1.5
+        tp.err_muti[0] = tp.err_muti[0] * 2.0
+    slab2, _ = case.slab()
+    c.analyze_var(other, slab2)
+    slab3, var3 = case.slab()
+    c.analyze_var(case.vp, slab3)
+    np.testing.assert_array_equal(var3.view(np.uint32), var1.view(np.uint32))
+    rel = increment_rel_rms(var1, case.var_out, case.var_in)
+    assert rel <= INCR_TOL, rel
