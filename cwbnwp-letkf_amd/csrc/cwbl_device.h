@@ -24,7 +24,7 @@ static __constant__ unsigned long long kExpT[32] = {
 
 // exp(real(4)) as the reference build evaluates it: glibc 2.35 expf, FMA variant
 // (table-driven, computed in double; the reference's flang `exp` calls libm expf).
-__device__ __forceinline__ float expf_ref(float x) {
+__device__ __forceinline__ float expf_ref(float x, const unsigned long long *tab = kExpT) {
   const unsigned ux = __float_as_uint(x);
   const unsigned abstop = (ux >> 20) & 0x7ffu;
   if (abstop >= 0x42bu) {  // |x| >= 88: not reached on this path (0.25*r2 <= 3.34)
@@ -41,7 +41,7 @@ __device__ __forceinline__ float expf_ref(float x) {
   const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
   kd = kd - shift;
   const double r = fma(invln2n, xd, -kd);
-  unsigned long long t = kExpT[ki & 31ull];
+  unsigned long long t = tab[ki & 31ull];
   t += ki << 47;
   const double s = __longlong_as_double((long long)t);
   const double z = fma(r, c0, c1);
@@ -65,8 +65,9 @@ __device__ __forceinline__ float gaspari_cohn(float x) {
 }
 
 // localisation weight on the error, module_letkf_core.f90:443-450 / 516-523
-__device__ __forceinline__ float error_inv(int wf, float err, float r2) {
-  if (wf != 1) return 1.0f / (err * expf_ref(0.25f * r2));
+__device__ __forceinline__ float error_inv(int wf, float err, float r2,
+                                           const unsigned long long *tab = kExpT) {
+  if (wf != 1) return 1.0f / (err * expf_ref(0.25f * r2, tab));
   return sqrtf(gaspari_cohn(sqrtf(r2))) / err;
 }
 
@@ -152,6 +153,28 @@ __device__ __forceinline__ double half_sum_dpp(double v) {
   return swap_add_f64<16>(row16_sum(v));
 }
 
+// Generic pointers held in structs (TreeDesc, SlabDev) are global memory; saying so lets the
+// compiler emit global_load (vector memory only) instead of flat loads, which also wait on
+// the LDS counter.
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T *gptr(const T *p) {
+  return (const __attribute__((address_space(1))) T *)p;
+}
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 gload4(const float *p) {  // 16-B global load
+  return *gptr(reinterpret_cast<const f32x4 *>(p));
+}
+// base[i] with a 32-bit byte offset (SGPR base + VGPR offset addressing); tables < 4 GiB
+template <class T>
+__device__ __forceinline__ T gld(const T *base, unsigned i) {
+  const char *b = reinterpret_cast<const char *>(base) + (unsigned)(i * (unsigned)sizeof(T));
+  return *gptr(reinterpret_cast<const T *>(b));
+}
+__device__ __forceinline__ f32x4 gld4(const float *base, unsigned i) {  // 16 B at base + 4i
+  const char *b = reinterpret_cast<const char *>(base) + (unsigned)(i * 4u);
+  return *gptr(reinterpret_cast<const f32x4 *>(b));
+}
+
 // Grid point g of a slab (the enumeration g = i + ix_lim*(j + iy_lim*kz) of the reference's
 // point loop, module_letkf_core.f90:209-213): projected x, y and altitude.
 __device__ __forceinline__ void slab_point(const SlabDev &s, long long g, float &x, float &y,
@@ -160,21 +183,20 @@ __device__ __forceinline__ void slab_point(const SlabDev &s, long long g, float 
   const long long r = g / s.ix_lim;
   const int j = (int)(r % s.iy_lim);
   const int kz = (int)(r / s.iy_lim);
-  x = s.x[i + (long long)s.nx * j];
-  y = s.y[i + (long long)s.nx * j];
-  z = s.alt[i + (long long)s.alt_nx * (j + (long long)s.alt_ny * kz)];
+  x = gptr(s.x)[i + (long long)s.nx * j];
+  y = gptr(s.y)[i + (long long)s.nx * j];
+  z = gptr(s.alt)[i + (long long)s.alt_nx * (j + (long long)s.alt_ny * kz)];
 }
 
-// Squared normalised distance of tree slot `slot` from the normalised query (q0, q1, q2),
-// evaluated exactly as the search does (process_terminal_node_fixedball,
+// Squared normalised distance of a tree point (rearranged coordinates d) from the normalised
+// query (q0, q1, q2), evaluated exactly as the search does (process_terminal_node_fixedball,
 // module_kdtree2.f90:1654-1707), so the solve reproduces the search's r2 bit for bit.
-__device__ __forceinline__ float slot_r2(const TreeDesc &T, int slot, float q0, float q1,
+__device__ __forceinline__ float slot_r2(const f32x4 d, int dim, float q0, float q1,
                                          float q2) {
-  const float4 d = T.rdata[slot];
   const float dx = d.x - q0, dy = d.y - q1;
   float sd = dx * dx;
   sd = sd + dy * dy;
-  if (T.tree_dim == 3) {
+  if (dim == 3) {
     const float dz = d.z - q2;
     sd = sd + dz * dz;
   }
@@ -191,8 +213,7 @@ template <int KP, int CHUNK>
 struct ColumnChunk {
   float yb[CHUNK][KP];
   float yo[CHUNK];
-  float w[CHUNK];
-  int col[CHUNK];
+  unsigned long long expt[32];  // expf table (kExpT) in LDS: per-lane lookups stay on chip
 };
 
 template <int KP>
@@ -202,9 +223,9 @@ struct AsmLayout {
   static constexpr int NBL = (NBLK + 63) / 64;      // blocks per lane
 };
 
-// Stages the point's accepted columns CHUNK at a time into `ch` (yb = bg * error_inv,
-// yo = omm * error_inv, in the reference's fp32 order) and calls accumulate(nsl) on each
-// staged chunk.  Returns the number of accepted columns (p).
+// Stages the point's columns CHUNK at a time into `ch` (yb = bg * error_inv,
+// yo = omm * error_inv, in the reference's fp32 order; rejected columns as zeros) and calls
+// accumulate(nsl) on each staged chunk.  Returns the number of accepted columns (p).
 template <int KP, int CHUNK, bool ASSEMBLED, class Acc>
 __device__ __forceinline__ int stage_columns(
     ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
@@ -214,53 +235,69 @@ __device__ __forceinline__ int stage_columns(
   const int k = c.k;
   int ptot = 0;
   if constexpr (!ASSEMBLED) {
+    if (lane < 32) ch.expt[lane] = kExpT[lane];
     for (int t = 0; t < c.ntrees; ++t) {
-      const TreeDesc &T = trees[t];
+      const TreeDesc T = trees[t];  // by value: the fields live in SGPRs for the whole loop
       // get_lz normalisation of the point (module_localization.f90:243-253), as the search
       const float q0 = pt.x * T.hclr_inv, q1 = pt.y * T.hclr_inv;
       const float q2 = T.query3d ? pt.z * T.vclr_inv : 0.0f;
-      const int cnt = nbr_cnt[(long long)gi * c.ntrees + t];
+      const int cnt = gptr(nbr_cnt)[(long long)gi * c.ntrees + t];
       const int nvar = T.nvar;
       const int npairs = cnt * nvar;
       const long long lbase = (long long)gi * c.list_cap + T.list_off;
+      // Candidate columns stay in the search's order; a rejected one is staged as a zero
+      // column (its bg row is zero and its weight 0), which adds exact zeros to every sum.
+      // So every gather of a chunk depends only on the neighbour slots: one round trip to
+      // memory per chunk, with the next chunk's slots prefetched behind it.  Lanes s and
+      // s + 32 stage column s of the chunk, half of its bg row each.
+      static_assert(CHUNK == 32, "two lanes per staged column");
+      constexpr int V4 = KP / 4, VH = V4 / 2;  // float4 per bg row, per lane
+      const int sl = lane & 31, half = lane >> 5;
+      const int *__restrict__ lst = nbr_idx + lbase;
+      int slot_next = 0;
+      if (sl < min(CHUNK, npairs)) slot_next = gld(lst, (unsigned)(sl / nvar));
       for (int base = 0; base < npairs; base += CHUNK) {
-        const int q = base + lane;
-        bool ok = false;
-        int col = 0;
+        const int nsl = min(CHUNK, npairs - base);
+        const bool live = sl < nsl;
+        const int q = base + sl;
+        const int jn = q / nvar, v = q - jn * nvar;
+        const int slot = slot_next;
+        const int col = slot * nvar + v;
+        uint8_t okb = 0;
+        float err = 1.0f, omm = 0.0f;
+        f32x4 rd = {0.0f, 0.0f, 0.0f, 0.0f};
+        f32x4 g[VH];
+#pragma unroll
+        for (int i = 0; i < VH; ++i) g[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if (live) {
+          okb = gld(T.col_ok, (unsigned)col);
+          err = gld(T.col_err, (unsigned)col);
+          omm = gld(T.col_omm, (unsigned)col);
+          rd = gld4(reinterpret_cast<const float *>(T.rdata), 4u * (unsigned)slot);
+          const unsigned b0 = (unsigned)(col * KP + 4 * VH * half);
+#pragma unroll
+          for (int i = 0; i < VH; ++i) g[i] = gld4(T.col_bg, b0 + 4u * i);
+        }
+        // prefetch the next chunk's slots behind this chunk's gathers
+        const int nb = base + CHUNK;
+        if (sl < min(CHUNK, npairs - nb)) slot_next = gld(lst, (unsigned)((nb + sl) / nvar));
+        const bool ok = live && okb != 0;
         float w = 0.0f, yo = 0.0f;
-        if (lane < CHUNK && q < npairs) {
-          const int jn = q / nvar, v = q - jn * nvar;
-          const int slot = nbr_idx[lbase + jn];
-          col = slot * nvar + v;
-          ok = T.col_ok[col] != 0;
-          if (ok) {
-            w = error_inv(c.weight_function, T.col_err[col], slot_r2(T, slot, q0, q1, q2));
-            yo = T.col_omm[col] * w;  // omm * error_inv (:451)
-          }
-        }
-        const unsigned long long mask = __ballot(ok);
-        const int nsl = __popcll(mask);
         if (ok) {
-          const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-          ch.col[pos] = col;
-          ch.w[pos] = w;
-          ch.yo[pos] = yo;
+          w = error_inv(c.weight_function, err, slot_r2(rd, T.tree_dim, q0, q1, q2), ch.expt);
+          yo = omm * w;  // omm * error_inv (:451)
         }
-        __syncthreads();
-        if (nsl == 0) continue;
-        constexpr int V4 = KP / 4;
-        for (int e = lane; e < nsl * V4; e += 64) {
-          const int s = e / V4, c4 = e - s * V4;
-          const float4 g = reinterpret_cast<const float4 *>(T.col_bg + (long long)ch.col[s] * KP)[c4];
-          const float ws = ch.w[s];
+        ptot += __popcll(__ballot(ok && half == 0));
+        if (half == 0) ch.yo[sl] = yo;
+        float *dst = &ch.yb[sl][4 * VH * half];
+#pragma unroll
+        for (int i = 0; i < VH; ++i) {
           float4 y;  // bg * error_inv (:452)
-          y.x = g.x * ws; y.y = g.y * ws; y.z = g.z * ws; y.w = g.w * ws;
-          *reinterpret_cast<float4 *>(&ch.yb[s][4 * c4]) = y;
+          y.x = g[i].x * w; y.y = g[i].y * w; y.z = g[i].z * w; y.w = g[i].w * w;
+          *reinterpret_cast<float4 *>(dst + 4 * i) = y;
         }
         __syncthreads();
         accumulate(nsl);
-        ptot += nsl;
         __syncthreads();
       }
     }
@@ -350,7 +387,7 @@ __device__ __forceinline__ void assemble_point_mfma(
   const int kk = lane >> 4, m = lane & 15;
   ptot = stage_columns<KP, CHUNK, ASSEMBLED>(
       ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in, [&](int nsl) {
-        for (int s0 = 0; s0 < nsl; s0 += 4) {
+        for (int s0 = 0; s0 < (c.debug_stop == 11 ? 0 : nsl); s0 += 4) {
           const int s = s0 + kk;
           const bool live = s < nsl;
           double op[L::NT];

@@ -257,7 +257,7 @@ hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, float r2, i
 // ---------------------------------------------------------------------------------------
 // solve_kernel<KP>: one wavefront (64 lanes) per grid point, members padded to KP
 // ---------------------------------------------------------------------------------------
-constexpr int kChunk = 64;      // columns staged per round
+constexpr int kChunk = 32;      // columns staged per round (two lanes per column)
 
 
 // Round-robin ("circle") tournament in slot form: slots (2i, 2i+1) form pair i; slot 0 is

@@ -4,10 +4,11 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/tqab_${TAG:-r1}
 mkdir -p $OUT
-for S in 0 1 2 3; do
+for S in ${STAGES:-0 1 2 3}; do
   CWBL_DEBUG_TQ_STOP=$S timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/stop$S.log 2>&1 || exit 4
   echo "stop=$S $(tail -1 $OUT/stop$S.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['detail']['ms_solve_per_step'])")"
 done
+[ -z "$PMC" ] && exit 0
 i=0
 for P in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
          "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_INSTS_SMEM SQ_INSTS_BRANCH" \
