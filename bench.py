@@ -136,6 +136,7 @@ def main():
         pts_total = float(pts_local)
 
     if rank == 0:
+        jacobi = os.environ.get("CWBL_SOLVER") == "jacobi"
         solved = sum(s.solved for s in stats)
         nobs_sum = sum(s.nobs_sum for s in stats)
         ms_solve = sum(s.ms_solve for s in stats)
@@ -177,16 +178,19 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK_TFLOPS,
                 "traffic": traffic,
-                "kernel": f"solve_kernel<{abi.MAX_MEMBERS if k > 56 else ((k + 7) // 8) * 8},false>",
+                "kernel": f"{'solve_kernel' if jacobi else 'solve_tq_kernel'}<{((k + 7) // 8) * 8},false>",
                 "note": "FP64 flops F(k,p) of SURVEY.md 8(d) per solve launch / HIP-event launch time (rank 0)",
             },
             "detail": {
+                "solver": "jacobi" if jacobi else "householder+quadrature",
                 "solved_per_step": solved / args.steps,
                 "ms_solve_per_step": ms_solve / args.steps,
                 "ms_search_per_step": ms_search / args.steps,
                 "ms_prep_per_step": sum(s.ms_prep for s in stats) / args.steps,
-                "max_sweeps": max(s.max_sweeps for s in stats),
-                "mean_sweeps": sum(s.sweeps_sum for s in stats) / max(solved, 1),
+                # Jacobi: sweeps; quadrature: decade of the spectrum bound (rule level)
+                ("max_sweeps" if jacobi else "max_quad_level"): max(s.max_sweeps for s in stats),
+                ("mean_sweeps" if jacobi else "mean_quad_level"):
+                    sum(s.sweeps_sum for s in stats) / max(solved, 1),
                 "nonconverged": sum(s.nonconverged for s in stats),
                 "obs_bcast_ms": bcast_ms,
             },

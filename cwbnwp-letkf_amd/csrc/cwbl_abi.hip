@@ -499,7 +499,8 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   B = std::max<long long>(std::min<long long>(B, npts), 256);
   B = std::min<long long>(B, 1 << 22);
   HIPCHK(S.nbr_cnt.ensure((size_t)B * nt * 4));
-  HIPCHK(S.nbr_idx.ensure((size_t)B * std::max(list_cap, 1) * 4));
+  HIPCHK(S.nbr_idx.ensure((size_t)((B + kListLanes - 1) / kListLanes) * kListLanes *
+                          std::max(list_cap, 1) * 4));
   HIPCHK(S.info.ensure((size_t)B * sizeof(int2)));
   HIPCHK(S.stats.ensure(sizeof(DevStats)));
   HIPCHK(hipMemsetAsync(S.stats.p, 0, sizeof(DevStats), S.stream));

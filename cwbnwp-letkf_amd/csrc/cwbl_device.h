@@ -244,7 +244,7 @@ __device__ __forceinline__ int stage_columns(
       const int cnt = gptr(nbr_cnt)[(long long)gi * c.ntrees + t];
       const int nvar = T.nvar;
       const int npairs = cnt * nvar;
-      const long long lbase = (long long)gi * c.list_cap + T.list_off;
+      const long long lbase = list_index(gi, c.list_cap, T.list_off);
       // Candidate columns stay in the search's order; a rejected one is staged as a zero
       // column (its bg row is zero and its weight 0), which adds exact zeros to every sum.
       // So every gather of a chunk depends only on the neighbour slots: one round trip to
@@ -255,7 +255,7 @@ __device__ __forceinline__ int stage_columns(
       const int sl = lane & 31, half = lane >> 5;
       const int *__restrict__ lst = nbr_idx + lbase;
       int slot_next = 0;
-      if (sl < min(CHUNK, npairs)) slot_next = gld(lst, (unsigned)(sl / nvar));
+      if (sl < min(CHUNK, npairs)) slot_next = gld(lst, (unsigned)(sl / nvar * kListLanes));
       for (int base = 0; base < npairs; base += CHUNK) {
         const int nsl = min(CHUNK, npairs - base);
         const bool live = sl < nsl;
@@ -280,7 +280,8 @@ __device__ __forceinline__ int stage_columns(
         }
         // prefetch the next chunk's slots behind this chunk's gathers
         const int nb = base + CHUNK;
-        if (sl < min(CHUNK, npairs - nb)) slot_next = gld(lst, (unsigned)((nb + sl) / nvar));
+        if (sl < min(CHUNK, npairs - nb))
+          slot_next = gld(lst, (unsigned)((nb + sl) / nvar * kListLanes));
         const bool ok = live && okb != 0;
         float w = 0.0f, yo = 0.0f;
         if (ok) {

@@ -128,6 +128,16 @@ hipError_t launch_reduce_info(hipStream_t s, const int2 *info, int n, DevStats *
 
 constexpr int kSearchStackDepth = 40;  // max k-d tree depth the search kernel supports
 
+// Neighbour lists of the analysis path are interleaved by groups of kListLanes points:
+// slot s of point g lives at list_index(g, cap, off) + s * kListLanes.  Lanes of one search
+// wave then write their lists side by side (whole cache lines) instead of 64 scattered
+// streams.  Buffers hold round_up(npts, kListLanes) * cap entries.
+constexpr int kListLanes = 64;
+__host__ __device__ inline long long list_index(long long g, int cap, int off) {
+  return (g / kListLanes) * (long long)cap * kListLanes + (long long)off * kListLanes +
+         (g % kListLanes);
+}
+
 int supported_kp(int k);      // smallest compiled KP >= k, or -1
 
 }  // namespace cwbl

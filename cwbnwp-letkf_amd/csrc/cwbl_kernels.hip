@@ -19,6 +19,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 namespace cwbl {
 
 // ---------------------------------------------------------------------------------------
@@ -147,7 +149,7 @@ __device__ int search_tree(const TreeDesc &T, float q0, float q1, float q2, floa
             out_idx[count] = T.ind[i];
             out_r2[count] = sd;
           } else {       // analysis: the tree slot (columns are stored in slot order)
-            out_idx[count] = i;
+            out_idx[(long long)count * kListLanes] = i;
           }
           ++count;
         }
@@ -222,7 +224,10 @@ search_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, floa
     // get_lz normalisation (module_localization.f90:243-253)
     const float q0 = px * T.hclr_inv, q1 = py * T.hclr_inv;
     const float q2 = T.query3d ? pz * T.vclr_inv : 0.0f;
-    const long long base = (long long)gi * list_cap + T.list_off;
+    // cwbl_search: one contiguous list per query; analysis: lists interleaved by wave
+    // (list_index), so the 64 lanes of a wave write slot c of their lists side by side
+    const long long base = nbr_r2 ? (long long)gi * list_cap + T.list_off
+                                  : list_index(gi, list_cap, T.list_off);
     bool ovf = false;
     int cnt = 0;
     if (T.max_lz > 0)
@@ -671,25 +676,25 @@ hipError_t launch_solve_assembled(hipStream_t s, int kp, SolveConsts c, int npts
                         col_off, yo, yb, xb, xa, evals, info);
 }
 
-// per-batch reduction of the per-point info into DevStats
-__global__ void __launch_bounds__(256)
+// per-batch reduction of the per-point info into DevStats: a grid-stride loop per block, a
+// block reduction through LDS, and one atomic per counter per block
+constexpr int kInfoThreads = 1024;
+__global__ void __launch_bounds__(kInfoThreads)
 reduce_info_kernel(const int2 *__restrict__ info, int n, DevStats *stats) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
   unsigned long long solved = 0, nobs = 0, noncv = 0, swsum = 0;
   unsigned int maxp = 0, maxsw = 0;
-  if (i < n) {
+  for (int i = blockIdx.x * kInfoThreads + threadIdx.x; i < n; i += gridDim.x * kInfoThreads) {
     const int2 v = info[i];
     if (v.x > 0) {
-      solved = 1;
-      nobs = (unsigned long long)v.x;
-      maxp = (unsigned)v.x;
+      solved += 1;
+      nobs += (unsigned long long)v.x;
+      maxp = max(maxp, (unsigned)v.x);
       const int sw = v.y < 0 ? -v.y : v.y;
-      maxsw = (unsigned)sw;
-      swsum = (unsigned long long)sw;
-      noncv = v.y < 0 ? 1 : 0;
+      maxsw = max(maxsw, (unsigned)sw);
+      swsum += (unsigned long long)sw;
+      noncv += v.y < 0 ? 1 : 0;
     }
   }
-  // wave reductions, one atomic per wave
   for (int off = 32; off > 0; off >>= 1) {
     solved += __shfl_xor(solved, off, 64);
     nobs += __shfl_xor(nobs, off, 64);
@@ -698,7 +703,20 @@ reduce_info_kernel(const int2 *__restrict__ info, int n, DevStats *stats) {
     maxp = max(maxp, (unsigned)__shfl_xor((int)maxp, off, 64));
     maxsw = max(maxsw, (unsigned)__shfl_xor((int)maxsw, off, 64));
   }
+  constexpr int NW = kInfoThreads / 64;
+  __shared__ unsigned long long red[4][NW];
+  __shared__ unsigned int redm[2][NW];
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
+    red[0][w] = solved; red[1][w] = nobs; red[2][w] = noncv; red[3][w] = swsum;
+    redm[0][w] = maxp; redm[1][w] = maxsw;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < NW; ++q) {
+      solved += red[0][q]; nobs += red[1][q]; noncv += red[2][q]; swsum += red[3][q];
+      maxp = max(maxp, redm[0][q]); maxsw = max(maxsw, redm[1][q]);
+    }
     if (solved) atomicAdd(&stats->solved, solved);
     if (nobs) atomicAdd(&stats->nobs_sum, nobs);
     if (noncv) atomicAdd(&stats->nonconverged, noncv);
@@ -710,7 +728,8 @@ reduce_info_kernel(const int2 *__restrict__ info, int n, DevStats *stats) {
 
 hipError_t launch_reduce_info(hipStream_t s, const int2 *info, int n, DevStats *stats) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(reduce_info_kernel, dim3((n + 255) / 256), dim3(256), 0, s, info, n,
+  const int blocks = std::min(256, (n + kInfoThreads - 1) / kInfoThreads);
+  hipLaunchKernelGGL(reduce_info_kernel, dim3(blocks), dim3(kInfoThreads), 0, s, info, n,
                      stats);
   return hipGetLastError();
 }

@@ -164,12 +164,14 @@ typedef struct cwbl_stats {
   long long solved;          /* points with >= 1 accepted obs (letkf_solve called) */
   long long nobs_sum;        /* sum of p over solved points */
   long long lz_truncated;    /* (point, type) searches that hit max_lz_pts (Q4) */
-  long long nonconverged;    /* eigensolves that hit the sweep cap (LAPACK info ignored, */
-                             /* module_eigen.f90:49) */
+  long long nonconverged;    /* Jacobi: eigensolves that hit the sweep cap (LAPACK info is */
+                             /* ignored, module_eigen.f90:49); quadrature: points whose */
+                             /* spectrum bound exceeds the last rule (max/min > 1e12) */
   long long q1_undefined;    /* (point, type) searches in the Q1 undefined case */
-  long long sweeps_sum;      /* Jacobi sweeps summed over solved points */
+  long long sweeps_sum;      /* solver effort summed over solved points: Jacobi sweeps, or */
+                             /* the quadrature rule's decade (default solver) */
   int       max_p;           /* max p over points */
-  int       max_sweeps;      /* max Jacobi sweeps used */
+  int       max_sweeps;      /* max of the same */
   int       ntrees;          /* trees built for this variable */
   int       reserved;
   double    ms_total;        /* wall time of the call */

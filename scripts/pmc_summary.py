@@ -2,7 +2,8 @@
 """Summarise a rocprofv3 run (kernel-trace stats + FETCH_SIZE / WRITE_SIZE passes) into
 profiles/<tag>_summary.json and profiles/pmc_solve_traffic.json (read by bench.py).
 
-HBM bytes per launch of the dominant kernel (solve_kernel) follow MI355X_MICROARCH.md
+HBM bytes per launch of the dominant kernel (solve_tq_kernel, or solve_kernel with
+CWBL_SOLVER=jacobi) follow MI355X_MICROARCH.md
 §HBM: FETCH_SIZE and WRITE_SIZE are in KiB, collected in separate passes; on gfx950
 FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads, so the corrected
 read bytes are 2 x FETCH_SIZE (an upper estimate for this kernel's mixed 4/16-B reads)."""
@@ -37,8 +38,11 @@ def main(src, tag):
             e["write_kib"] = write.get(k)
             e["hbm_bytes_per_launch_corrected"] = (2 * fetch[k] + (write.get(k) or 0)) * 1024
         out["kernels"][k] = e
-    solve = [k for k in out["kernels"] if "solve_kernel" in k][0]
+    names = list(out["kernels"])
+    solve = ([k for k in names if "solve_tq_kernel" in k] or [k for k in names if "solve_kernel" in k])[0]
     os.makedirs("profiles", exist_ok=True)
+    import shutil
+    shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), f"profiles/{tag}_kernel_stats.csv")
     json.dump(out, open(f"profiles/{tag}_summary.json", "w"), indent=1)
     json.dump({"kernel": solve, "tag": tag,
                "hbm_bytes_per_launch": out["kernels"][solve]["hbm_bytes_per_launch_corrected"],
