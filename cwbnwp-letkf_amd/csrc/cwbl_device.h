@@ -148,6 +148,31 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
   return swap_add_f64<32>(swap_add_f64<16>(row16_sum(v)));
 }
 
+// Four wave sums at once: two transposing stages (v_permlane32_swap, v_permlane16_swap)
+// leave row r of the wave holding partial sums of value r, a row reduction finishes them,
+// and lanes 0/16/32/48 hand the results out as wave-uniform values.  29 instructions for
+// four sums instead of 4 x 22.
+__device__ __forceinline__ void wave_sum4_dpp(double &a, double &b, double &c, double &d) {
+  auto lo = [](double x) { return (int)__double_as_longlong(x); };
+  auto hi = [](double x) { return (int)(__double_as_longlong(x) >> 32); };
+  auto mk = [](int l, int h) { return __longlong_as_double(((long long)h << 32) | (unsigned)l); };
+  // lanes 0-31: a[i] + a[i+32], lanes 32-63: c[i-32] + c[i]; same for (b, d)
+  auto s1l = __builtin_amdgcn_permlane32_swap(lo(a), lo(c), false, false);
+  auto s1h = __builtin_amdgcn_permlane32_swap(hi(a), hi(c), false, false);
+  auto s2l = __builtin_amdgcn_permlane32_swap(lo(b), lo(d), false, false);
+  auto s2h = __builtin_amdgcn_permlane32_swap(hi(b), hi(d), false, false);
+  const double r1 = mk(s1l[0], s1h[0]) + mk(s1l[1], s1h[1]);
+  const double r2 = mk(s2l[0], s2h[0]) + mk(s2l[1], s2h[1]);
+  // even rows: r1[i] + r1[i+16], odd rows: r2[i-16] + r2[i] -> row 0 a, 1 b, 2 c, 3 d
+  auto tl = __builtin_amdgcn_permlane16_swap(lo(r1), lo(r2), false, false);
+  auto th = __builtin_amdgcn_permlane16_swap(hi(r1), hi(r2), false, false);
+  const double r = row16_sum(mk(tl[0], th[0]) + mk(tl[1], th[1]));
+  a = readlane_f64(r, 0);
+  b = readlane_f64(r, 16);
+  c = readlane_f64(r, 32);
+  d = readlane_f64(r, 48);
+}
+
 // Sum over each half wave (lanes 0-31, 32-63); every lane gets its half's sum.
 __device__ __forceinline__ double half_sum_dpp(double v) {
   return swap_add_f64<16>(row16_sum(v));

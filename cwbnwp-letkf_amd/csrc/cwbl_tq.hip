@@ -236,7 +236,9 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     }
     const double x = (lane > j + 1 && lane < k) ? sm.col[lane] : 0.0;
     const double alpha = sm.col[j + 1];
-    const double xn2 = wave_sum_dpp(x * x);
+    // x.x, x.ux, x.ub in one pass: v = x * scal + e_{j+1} gives v.u = scal (x.u) + u_{j+1}
+    double xn2 = x * x, xux = x * ux, xub = x * ub, pad = 0.0;
+    wave_sum4_dpp(xn2, xux, xub, pad);
     double tau = 0.0, beta = alpha, scal = 0.0;
     if (xn2 > 0.0) {  // dlarfg, with fp64 rcp/rsq refined to ~1 ulp
       const double a2 = fma(alpha, alpha, xn2);
@@ -253,8 +255,8 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     const double v = lane == j + 1 ? 1.0 : x * scal;
     if (lane < KP) sm.vb[lane] = v;
     if (lane > j && lane < k) sm.u.reg[SM::hv_off(0) + j * (k - 1) - j * (j - 1) / 2 + lane - (j + 1)] = v;
-    const double s2 = wave_sum_dpp(v * ux);
-    const double s3 = wave_sum_dpp(v * ub);
+    const double s2 = fma(scal, xux, readlane_f64(ux, j + 1));  // v . ux
+    const double s3 = fma(scal, xub, readlane_f64(ub, j + 1));  // v . ub
     ux = fma(-tau * s2, v, ux);
     ub = fma(-tau * s3, v, ub);
     __syncthreads();
