@@ -32,7 +32,7 @@ namespace cwbl {
 
 constexpr int kTqChunk = 32;  // columns staged per round
 
-// LDS of one point (KP = 40: 9.8 KB, so 16 waves fit a CU).  The big union is reused by
+// LDS of one point (KP = 40: 9.4 KB, so 16 waves fit a CU).  The big union is reused by
 // phase: staged columns -> half of A -> {Householder vectors + A v partials}, then
 // {Householder vectors + Q^T b1, Q^T x', T^-1/2 u2}.  The A v partials of step j only need
 // block rows >= j/4 and sit at the top of the region, above the Householder vectors
@@ -66,9 +66,6 @@ struct TqSmem {
   // reads a row with one address; record KP only holds c(KP-1,KP) = 0
   double tq[KP + 1][4];                   // d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
   double tau[KP];                         // Householder scalars
-  float xb[KP], xa[KP];
-  double scal[4];
-  float fscal[4];
 };
 
 // waves per SIMD the register allocation is held to (VGPR budget 512 / waves)
@@ -98,6 +95,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
 
   long long P = 0;  // var index of member 0
   float3 pt = make_float3(0.0f, 0.0f, 0.0f);  // the point's projected x, y and altitude
+  float xbl = 0.0f;                            // background of member `lane`
   if constexpr (!ASSEMBLED) {
     const long long g = g0 + gi;
     const int i = (int)(g % slab.ix_lim);
@@ -105,10 +103,10 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     const int j = (int)(r % slab.iy_lim);
     const int kz = (int)(r / slab.iy_lim);
     P = i + (long long)slab.nx * (j + (long long)slab.ny * kz);
-    if (lane < KP) sm.xb[lane] = lane < k ? slab.var[P + slab.L * lane] : 0.0f;
+    if (lane < k) xbl = slab.var[P + slab.L * lane];
     slab_point(slab, g, pt.x, pt.y, pt.z);
   } else {
-    if (lane < KP) sm.xb[lane] = lane < k ? xb_in[(long long)gi * k + lane] : 0.0f;
+    if (lane < k) xbl = xb_in[(long long)gi * k + lane];
   }
 
   f64x4 tile[MfmaLayout<KP>::NTL];
@@ -121,7 +119,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   if (ptot == 0) {  // no accepted observation: var left unchanged (:220, :226)
     if (lane == 0 && info) info[gi] = make_int2(0, 0);
     if constexpr (ASSEMBLED) {
-      if (lane < k) xa_out[(long long)gi * k + lane] = sm.xb[lane];
+      if (lane < k) xa_out[(long long)gi * k + lane] = xbl;
     }
     return;
   }
@@ -181,11 +179,6 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
       }
     }
   }
-  if (lane == 0) {  // xb_mean = sum(xb) * nmember_inv in fp32 (:671)
-    float s = 0.0f;
-    for (int mm = 0; mm < k; ++mm) s = s + sm.xb[mm];
-    sm.scal[0] = (double)(s * c.nmember_inv);
-  }
   if (lane < KP) {  // padding of T: decoupled unit rows
     sm.tq[lane][0] = 1.0;
     sm.tq[lane][1] = 0.0;
@@ -193,8 +186,14 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   }
   if (lane == 0) sm.tq[KP][1] = 0.0;
   __syncthreads();
-  const double xb_mean = sm.scal[0];
-  double ux = (lane < k) ? (double)sm.xb[lane] - xb_mean : 0.0;  // x', becomes Q^T x'
+  double xb_mean;
+  {  // xb_mean = sum(xb) * nmember_inv in fp32 (:671), sequential like the reference
+    float s = 0.0f;
+    for (int mm = 0; mm < k; ++mm)
+      s = s + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xbl), mm));
+    xb_mean = (double)(s * c.nmember_inv);
+  }
+  double ux = (lane < k) ? (double)xbl - xb_mean : 0.0;  // x', becomes Q^T x'
   double ub = (lane < KP) ? b1acc : 0.0;                          // Yb d, becomes Q^T b1
 
   // ---- Householder tridiagonalisation (lower, dsytd2 order) ------------------------------
@@ -410,60 +409,64 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     if (lane == 0 && info) info[gi] = make_int2(ptot, (int)d);
     return;
   }
-  // ---- back-transform: y <- Q y = H_0 H_1 ... H_{k-3} y -----------------------------------
-  for (int j = k - 3; j >= 0; --j) {
-    const double tj = sm.tau[j];
-    if (tj == 0.0) continue;
+  // ---- back-transform: y <- Q y = H_0 H_1 ... H_{k-3} y, two reflectors per reduction ----
+  // H_{j-1} H_j y: a = v_j.y, b = v_{j-1}.y, c = v_{j-1}.v_j (one 4-value reduction), then
+  // y -= tau_j a v_j and y -= tau_{j-1} (b - tau_j a c) v_{j-1}.
+  auto hvec = [&](int j) {
     const int off = j * (k - 1) - j * (j - 1) / 2;
-    const double vj = (lane > j && lane < k) ? sm.u.reg[off + lane - (j + 1)] : 0.0;
-    const double s = wave_sum_dpp(vj * yl);
-    yl = fma(-tj * s, vj, yl);
+    return (lane > j && lane < k) ? sm.u.reg[off + lane - (j + 1)] : 0.0;
+  };
+  int j = k - 3;
+  for (; j >= 1; j -= 2) {
+    const double t1 = sm.tau[j], t0 = sm.tau[j - 1];
+    // a reflector with tau = 0 was never stored (H = I): use a zero vector
+    const double v1 = t1 == 0.0 ? 0.0 : hvec(j), v0 = t0 == 0.0 ? 0.0 : hvec(j - 1);
+    double a1 = v1 * yl, b0 = v0 * yl, c01 = v0 * v1, pad = 0.0;
+    wave_sum4_dpp(a1, b0, c01, pad);
+    yl = fma(-t1 * a1, v1, yl);
+    yl = fma(-t0 * fma(-t1 * a1, c01, b0), v0, yl);
+  }
+  if (j == 0 && sm.tau[0] != 0.0) {
+    const double v0 = hvec(0);
+    const double s0 = wave_sum_dpp(v0 * yl);
+    yl = fma(-sm.tau[0] * s0, v0, yl);
   }
   const double sk = sqrt((double)(k - 1));
-  if (lane < KP) sm.xa[lane] = (float)(xb_mean + (d + sk * yl));  // xa = wbar (:675-679)
-  __syncthreads();
+  // analysis of member `lane` (xa = wbar, :675-679); fp32 from here on, in registers
+  float xal = lane < KP ? (float)(xb_mean + (d + sk * yl)) : 0.0f;
 
   // ---- RTPP / RTPS (:684-698), fp32 in the reference's order -------------------------
+  // the reference's sequential sums run on wave-uniform values read lane by lane
+  auto seq_sum = [&](float x) {
+    float s = 0.0f;
+    for (int mm = 0; mm < k; ++mm) s = s + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), mm));
+    return s;
+  };
   if (c.use_rtpp || c.use_rtps) {
-    if (lane == 0) {
-      float s = 0.0f;
-      for (int mm = 0; mm < k; ++mm) s = s + sm.xa[mm];
-      sm.fscal[0] = s * c.nmember_inv;  // xa_mean
-    }
-    __syncthreads();
-    const float xa_mean = sm.fscal[0];
-    const double xpl = lane < k ? (double)sm.xb[lane] - xb_mean : 0.0;
+    const float xa_mean = seq_sum(xal) * c.nmember_inv;
+    const double xpl = lane < k ? (double)xbl - xb_mean : 0.0;
     float xap = 0.0f;
     if (lane < k) {
-      xap = sm.xa[lane] - xa_mean;
+      xap = xal - xa_mean;
       if (c.use_rtpp)
         xap = (float)((double)((1.0f - c.rtpp_alpha) * xap) + (double)c.rtpp_alpha * xpl);
     }
     if (c.use_rtps) {
-      __syncthreads();
-      if (lane < k) sm.xa[lane] = xap;  // stage xa_prime
-      __syncthreads();
-      if (lane == 0) {
-        double d8 = 0.0;
-        for (int mm = 0; mm < k; ++mm) {
-          const double xp = (double)sm.xb[mm] - xb_mean;
-          d8 = d8 + xp * xp;
-        }
-        const float xb_std = (float)d8;
-        float xa_std = 0.0f;
-        for (int mm = 0; mm < k; ++mm) xa_std = xa_std + sm.xa[mm] * sm.xa[mm];
-        sm.fscal[1] = c.rtps_alpha * sqrtf(xb_std / xa_std) - c.rtps_alpha + 1.0f;
+      double d8 = 0.0;
+      for (int mm = 0; mm < k; ++mm) {
+        const double xp = readlane_f64(xpl, mm);
+        d8 = d8 + xp * xp;
       }
-      __syncthreads();
-      xap = xap * sm.fscal[1];
+      const float xb_std = (float)d8;
+      const float xa_std = seq_sum(xap * xap);
+      xap = xap * (c.rtps_alpha * sqrtf(xb_std / xa_std) - c.rtps_alpha + 1.0f);
     }
-    if (lane < k) sm.xa[lane] = xa_mean + xap;
-    __syncthreads();
+    xal = xa_mean + xap;
   }
 
   if (lane < k) {
-    if constexpr (ASSEMBLED) xa_out[(long long)gi * k + lane] = sm.xa[lane];
-    else slab.var[P + slab.L * lane] = sm.xa[lane];
+    if constexpr (ASSEMBLED) xa_out[(long long)gi * k + lane] = xal;
+    else slab.var[P + slab.L * lane] = xal;
   }
   // info.y: decade of the quadrature rule (negative when M/m exceeds the last table)
   if (lane == 0 && info) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
