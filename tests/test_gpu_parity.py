@@ -246,3 +246,37 @@ def test_tree_cache_across_variables():
     np.testing.assert_array_equal(var3.view(np.uint32), var1.view(np.uint32))
     rel = increment_rel_rms(var1, case.var_out, case.var_in)
     assert rel <= INCR_TOL, rel
+
+
+def test_dense_radar_c5_block_vs_oracle():
+    """C5-shaped dense radar (dbz-like type, ~2000 local obs per point, max_lz 4000) on a
+    30x30x60 cut of the 600x600x60 grid: GPU vs the oracle on a 6x6-column block.  A fifth
+    of the obs are `norain` (some with all-norain backgrounds) to exercise the dbz rules
+    (module_letkf_core.f90:504-507)."""
+    import ctypes as C
+    from cwbl import synth
+    w = synth.make("c5", scale=0.05)
+    norain = -5.0
+    rng = np.random.default_rng(5)
+    sel = rng.random(w.obs.shape[0]) < 0.2
+    w.obs[sel] = norain
+    allrain = sel & (rng.random(w.obs.shape[0]) < 0.5)
+    w.hdxb[:, allrain] = norain
+    c = core(w.k, 0, norain)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    var = w.var.copy()
+    st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+    assert np.isfinite(var).all()
+    assert st.nonconverged == 0
+    mean_p = st.nobs_sum / max(st.solved, 1)
+    assert 600 <= mean_p <= 4000, mean_p
+    j0, i0, nb = 12, 12, 6
+    sub = lambda a: np.ascontiguousarray(a[..., j0:j0 + nb, i0:i0 + nb])  # noqa: E731
+    ref = sub(w.var).copy()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    rc = oracle().orc_analyze_var(w.k, 0, norain, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(sub(w.x), sub(w.y), sub(w.alt), ref)),
+                                  16, C.byref(abi.Stats()))
+    assert rc == 0
+    rel = increment_rel_rms(sub(var), ref, sub(w.var))
+    assert rel <= INCR_TOL, rel
