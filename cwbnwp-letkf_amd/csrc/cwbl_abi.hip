@@ -520,7 +520,11 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     HIPCHK(launch_search(S.stream, dtrees, nt, list_cap, c.r2, sd, g0, nb,
                          S.nbr_cnt.as<int>(), S.nbr_idx.as<int>(), nullptr, dst));
     HIPCHK(hipEventRecord(b, S.stream));
-    if (S.jacobi)
+    if (S.kp > kMaxWaveKP)
+      HIPCHK(launch_solve_tq_big(S.stream, S.kp, false, dtrees, c, sd, g0, nb,
+                                 S.nbr_cnt.as<int>(), S.nbr_idx.as<int>(), nullptr, nullptr,
+                                 nullptr, nullptr, nullptr, S.info.as<int2>()));
+    else if (S.jacobi)
       HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, S.nbr_cnt.as<int>(),
                                     S.nbr_idx.as<int>(), S.info.as<int2>()));
     else
@@ -565,6 +569,9 @@ int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const 
   if (npts < 0 || (npts > 0 && (!col_off || !xb || !xa)))
     return fail(CWBL_ERR_ARG, "cwbl_solve_batch: bad arguments");
   if (npts == 0) return CWBL_OK;
+  if (evals && S.kp > kMaxWaveKP)
+    return fail(CWBL_ERR_UNSUPPORTED,
+                "cwbl_solve_batch: eigenvalue output needs k <= %d (the Jacobi path)", kMaxWaveKP);
   const size_t k = (size_t)S.k;
   std::vector<long long> hoff;
   const long long *doff = col_off;
@@ -592,7 +599,10 @@ int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const 
   }
   HIPCHK(S.info.ensure((size_t)npts * sizeof(int2)));
   SolveConsts c = solve_consts(inflat, use_rtpp, rtpp_alpha, use_rtps, rtps_alpha);
-  if (dev || S.jacobi)  // eigenvalues requested: the Jacobi eigensolver path
+  if (S.kp > kMaxWaveKP)
+    HIPCHK(launch_solve_tq_big(S.stream, S.kp, true, nullptr, c, SlabDev{}, 0, npts, nullptr,
+                               nullptr, doff, dyo, dyb, dxb, dxa, S.info.as<int2>()));
+  else if (dev || S.jacobi)  // eigenvalues requested: the Jacobi eigensolver path
     HIPCHK(launch_solve_assembled(S.stream, S.kp, c, npts, doff, dyo, dyb, dxb, dxa, dev,
                                   S.info.as<int2>()));
   else

@@ -241,17 +241,18 @@ struct ColumnChunk {
   unsigned long long expt[32];  // expf table (kExpT) in LDS: per-lane lookups stay on chip
 };
 
-template <int KP>
+template <int KP, int NT = 64>
 struct AsmLayout {
   static constexpr int NB = KP / 4;                 // 4x4 blocks per dimension
   static constexpr int NBLK = NB * (NB + 1) / 2;    // lower-triangle blocks
-  static constexpr int NBL = (NBLK + 63) / 64;      // blocks per lane
+  static constexpr int NBL = (NBLK + NT - 1) / NT;  // blocks per thread (NT threads per point)
 };
 
 // Stages the point's columns CHUNK at a time into `ch` (yb = bg * error_inv,
 // yo = omm * error_inv, in the reference's fp32 order; rejected columns as zeros) and calls
-// accumulate(nsl) on each staged chunk.  Returns the number of accepted columns (p).
-template <int KP, int CHUNK, bool ASSEMBLED, class Acc>
+// accumulate(nsl) on each staged chunk.  NT threads per point (`lane` = thread index).
+// Returns the number of accepted columns (p); with NT > 64 the count is valid in wave 0.
+template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64, class Acc>
 __device__ __forceinline__ int stage_columns(
     ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
@@ -273,10 +274,12 @@ __device__ __forceinline__ int stage_columns(
       // Candidate columns stay in the search's order; a rejected one is staged as a zero
       // column (its bg row is zero and its weight 0), which adds exact zeros to every sum.
       // So every gather of a chunk depends only on the neighbour slots: one round trip to
-      // memory per chunk, with the next chunk's slots prefetched behind it.  Lanes s and
-      // s + 32 stage column s of the chunk, half of its bg row each.
-      static_assert(CHUNK == 32, "two lanes per staged column");
-      constexpr int V4 = KP / 4, VH = V4 / 2;  // float4 per bg row, per lane
+      // memory per chunk, with the next chunk's slots prefetched behind it.  Threads s,
+      // s + 32, s + 64, ... stage column s of the chunk, a part of its bg row each.
+      static_assert(CHUNK == 32, "32 staged columns per round");
+      constexpr int LPC = NT / 32;                       // threads per staged column
+      constexpr int V4 = KP / 4, VH = V4 / LPC;          // float4 per bg row, per thread
+      static_assert(V4 % LPC == 0, "bg row split");
       const int sl = lane & 31, half = lane >> 5;
       const int *__restrict__ lst = nbr_idx + lbase;
       int slot_next = 0;
@@ -313,7 +316,7 @@ __device__ __forceinline__ int stage_columns(
           w = error_inv(c.weight_function, err, slot_r2(rd, T.tree_dim, q0, q1, q2), ch.expt);
           yo = omm * w;  // omm * error_inv (:451)
         }
-        ptot += __popcll(__ballot(ok && half == 0));
+        ptot += __popcll(__ballot(ok && half == 0));  // counted by wave 0
         if (half == 0) ch.yo[sl] = yo;
         float *dst = &ch.yb[sl][4 * VH * half];
 #pragma unroll
@@ -333,7 +336,7 @@ __device__ __forceinline__ int stage_columns(
     for (int base = 0; base < ncol; base += CHUNK) {
       const int nsl = min(CHUNK, ncol - base);
       if (lane < nsl) ch.yo[lane] = yo_in[c0 + base + lane];
-      for (int e = lane; e < nsl * KP; e += 64) {
+      for (int e = lane; e < nsl * KP; e += NT) {
         const int s = e / KP, m = e - s * KP;
         ch.yb[s][m] = m < k ? yb_in[(c0 + base + s) * k + m] : 0.0f;
       }
@@ -346,28 +349,28 @@ __device__ __forceinline__ int stage_columns(
   return ptot;
 }
 
-// Column assembly on the VALU: lane L accumulates the 4x4 blocks L, L+64, ... of the lower
-// block triangle of Yb Yb^T, and lanes < KP the entries of Yb d.
-template <int KP, int CHUNK, bool ASSEMBLED>
+// Column assembly on the VALU: thread L accumulates the 4x4 blocks L, L+NT, ... of the lower
+// block triangle of Yb Yb^T, and threads < KP the entries of Yb d.
+template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64>
 __device__ __forceinline__ void assemble_point(
     ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
     const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in,
-    const int (&bi)[AsmLayout<KP>::NBL], const int (&bj)[AsmLayout<KP>::NBL],
-    double (&acc)[AsmLayout<KP>::NBL][16], double &b1acc, int &ptot) {
-  constexpr int NBL = AsmLayout<KP>::NBL, NBLK = AsmLayout<KP>::NBLK;
+    const int (&bi)[AsmLayout<KP, NT>::NBL], const int (&bj)[AsmLayout<KP, NT>::NBL],
+    double (&acc)[AsmLayout<KP, NT>::NBL][16], double &b1acc, int &ptot) {
+  constexpr int NBL = AsmLayout<KP, NT>::NBL, NBLK = AsmLayout<KP, NT>::NBLK;
 #pragma unroll
   for (int it = 0; it < NBL; ++it)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[it][e] = 0.0;
   b1acc = 0.0;
-  ptot = stage_columns<KP, CHUNK, ASSEMBLED>(
+  ptot = stage_columns<KP, CHUNK, ASSEMBLED, NT>(
       ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in, [&](int nsl) {
         for (int s = 0; s < nsl; ++s) {
 #pragma unroll
           for (int it = 0; it < NBL; ++it) {
-            if (lane + 64 * it < NBLK) {
+            if (lane + NT * it < NBLK) {
               const float4 ra = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bi[it]]);
               const float4 rb = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bj[it]]);
               const double a4[4] = {ra.x, ra.y, ra.z, ra.w};
@@ -441,13 +444,13 @@ __device__ __forceinline__ void assemble_point_mfma(
       });
 }
 
-// lane -> 4x4 block (bi, bj) of the lower block triangle, row-major over the triangle
-template <int KP>
-__device__ __forceinline__ void block_of_lane(int lane, int (&bi)[AsmLayout<KP>::NBL],
-                                              int (&bj)[AsmLayout<KP>::NBL]) {
+// thread -> 4x4 block (bi, bj) of the lower block triangle, row-major over the triangle
+template <int KP, int NT = 64>
+__device__ __forceinline__ void block_of_lane(int lane, int (&bi)[AsmLayout<KP, NT>::NBL],
+                                              int (&bj)[AsmLayout<KP, NT>::NBL]) {
 #pragma unroll
-  for (int it = 0; it < AsmLayout<KP>::NBL; ++it) {
-    const int b = lane + 64 * it;
+  for (int it = 0; it < AsmLayout<KP, NT>::NBL; ++it) {
+    const int b = lane + NT * it;
     int rr = 0;
     while ((rr + 1) * (rr + 2) / 2 <= b) ++rr;
     bi[it] = rr;

@@ -120,6 +120,13 @@ hipError_t launch_solve_tq(hipStream_t s, int kp, bool assembled, const TreeDesc
                            const long long *col_off, const float *yo, const float *yb,
                            const float *xb, float *xa, int2 *info);
 
+// KP = 96, 128: one 256-thread workgroup per point (cwbl_tq_big.hip)
+hipError_t launch_solve_tq_big(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,
+                               SolveConsts c, SlabDev slab, long long g0, int npts,
+                               const int *nbr_cnt, const int *nbr_idx,
+                               const long long *col_off, const float *yo, const float *yb,
+                               const float *xb, float *xa, int2 *info);
+
 hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, float r2, int nq,
                                 const float *q_xyz, int max_lz, int *nfound, int *idx,
                                 float *r2out);
@@ -139,5 +146,6 @@ __host__ __device__ inline long long list_index(long long g, int cap, int off) {
 }
 
 int supported_kp(int k);      // smallest compiled KP >= k, or -1
+constexpr int kMaxWaveKP = 64;  // largest KP of the one-wavefront kernels
 
 }  // namespace cwbl

@@ -627,7 +627,9 @@ static hipError_t launch_solve_kp(hipStream_t s, bool assembled, const TreeDesc 
   return hipGetLastError();
 }
 
-static const int kSupportedKP[] = {8, 16, 24, 32, 40, 48, 56, 64};
+// KP <= 64: one wavefront per point (solve_tq_kernel, solve_kernel); 96 and 128: one
+// 256-thread workgroup per point (solve_tq_big_kernel; no Jacobi eigenvalue path)
+static const int kSupportedKP[] = {8, 16, 24, 32, 40, 48, 56, 64, 96, 128};
 
 int supported_kp(int k) {
   for (int kp : kSupportedKP)

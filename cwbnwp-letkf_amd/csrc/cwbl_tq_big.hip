@@ -1,0 +1,475 @@
+// cwbl_tq_big.hip — solve_tq_big_kernel<KP>: the Householder + quadrature solve of
+// cwbl_tq.hip for large ensembles (KP = 96, 128; configs[3] is k = 128), one 256-thread
+// workgroup (4 waves) per grid point.
+//
+// Same algorithm as solve_tq_kernel (see there for the derivation and the reference lines);
+// what changes with k:
+//   - the k x k matrix lives in 4x4 register blocks spread over 256 threads (NBL blocks per
+//     thread), assembled on the VALU (the MFMA tile set of Y'Y'^T would not fit in registers);
+//   - reductions are wave reductions followed by a 4-entry exchange through LDS;
+//   - the Householder vectors are kept in registers, in the entries of column j that the
+//     tridiagonalisation no longer reads (rows > j+1 of block column j/4), and published
+//     again for the back-transform;
+//   - the shifted tridiagonal solves of the quadrature run on wave 0 (lane pairs, twisted
+//     factorisation) with the forward sweep checkpointed every 8 rows and recomputed per
+//     segment in the backward sweep, so a lane holds 64 rows in 64 VGPRs;
+//   - the reference's sequential fp32 member sums run wave after wave.
+#include "cwbl_device.h"
+
+namespace cwbl {
+
+constexpr int kBigThreads = 256;
+constexpr int kBigChunk = 32;
+
+template <int KP>
+struct BigSmem {
+  static constexpr int NB = KP / 4;
+  static constexpr int PLD = 4 * NB + 4;  // 2*PLD = 8*odd dwords: conflict-free row sums
+  union {
+    ColumnChunk<KP, kBigChunk> ch;
+    double pb[NB][PLD];                   // A v partials: pb[R][4c+r] = block (R,c), row r
+  } u;
+  double col[KP];                         // pivot column / reflector j (back-transform)
+  double col2[KP];                        // reflector j-1 (back-transform)
+  double vb[KP], wb[KP];                  // v and w of the current step; Yb d before
+  double tq[KP + 1][4];                   // d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
+  double Ym[KP], Zm[KP];                  // quadrature sum / exact solve, walk order
+  double tau[KP];
+  double red[2][4][4];                    // [buffer][wave][value] of the block reductions
+  double pard;                            // sequential-sum partial handed wave to wave
+  float parf;
+  int ptot;
+};
+
+template <int KP, bool ASSEMBLED>
+__global__ void __launch_bounds__(kBigThreads)
+solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
+                    long long g0, int npts, const int *__restrict__ nbr_cnt,
+                    const int *__restrict__ nbr_idx, const long long *__restrict__ col_off,
+                    const float *__restrict__ yo_in, const float *__restrict__ yb_in,
+                    const float *__restrict__ xb_in, float *__restrict__ xa_out,
+                    int2 *__restrict__ info) {
+  constexpr int NT = kBigThreads;
+  constexpr int H = KP / 2;
+  using L = AsmLayout<KP, NT>;
+  constexpr int NBL = L::NBL, NBLK = L::NBLK;
+  using SM = BigSmem<KP>;
+  static_assert(KP % 8 == 0 && KP <= 2 * 64 && H % 8 == 0, "KP");
+  __shared__ SM sm;
+
+  const int gi = xcd_remap(blockIdx.x, gridDim.x);
+  if (gi >= npts) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int k = c.k;
+
+  // ---- block reductions: 4 values, wave sums + exchange through LDS (one barrier) ---------
+  int rbuf = 0;
+  auto bsum4 = [&](double &a, double &b, double &cc, double &d) {
+    wave_sum4_dpp(a, b, cc, d);
+    double(*r)[4] = sm.red[rbuf];
+    rbuf ^= 1;
+    if (lane == 0) {
+      r[wave][0] = a; r[wave][1] = b; r[wave][2] = cc; r[wave][3] = d;
+    }
+    __syncthreads();
+    a = (r[0][0] + r[1][0]) + (r[2][0] + r[3][0]);
+    b = (r[0][1] + r[1][1]) + (r[2][1] + r[3][1]);
+    cc = (r[0][2] + r[1][2]) + (r[2][2] + r[3][2]);
+    d = (r[0][3] + r[1][3]) + (r[2][3] + r[3][3]);
+  };
+  // the reference's sequential member-order sums (member m lives in thread m), wave by wave
+  auto seq_sum_f32 = [&](float x) {
+    for (int w = 0; 64 * w < k; ++w) {
+      if (wave == w) {
+        float s = w == 0 ? 0.0f : sm.parf;
+        const int n = min(64, k - 64 * w);
+        for (int m = 0; m < n; ++m)
+          s = s + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), m));
+        if (lane == 0) sm.parf = s;
+      }
+      __syncthreads();
+    }
+    const float s = sm.parf;
+    __syncthreads();
+    return s;
+  };
+  auto seq_sumsq_f64 = [&](double x) {
+    for (int w = 0; 64 * w < k; ++w) {
+      if (wave == w) {
+        double s = w == 0 ? 0.0 : sm.pard;
+        const int n = min(64, k - 64 * w);
+        for (int m = 0; m < n; ++m) {
+          const double v = readlane_f64(x, m);
+          s = s + v * v;
+        }
+        if (lane == 0) sm.pard = s;
+      }
+      __syncthreads();
+    }
+    const double s = sm.pard;
+    __syncthreads();
+    return s;
+  };
+
+  long long P = 0;
+  float3 pt = make_float3(0.0f, 0.0f, 0.0f);
+  float xbl = 0.0f;  // background of member `tid`
+  if constexpr (!ASSEMBLED) {
+    const long long g = g0 + gi;
+    const int i = (int)(g % slab.ix_lim);
+    const long long r = g / slab.ix_lim;
+    const int j = (int)(r % slab.iy_lim);
+    const int kz = (int)(r / slab.iy_lim);
+    P = i + (long long)slab.nx * (j + (long long)slab.ny * kz);
+    if (tid < k) xbl = slab.var[P + slab.L * tid];
+    slab_point(slab, g, pt.x, pt.y, pt.z);
+  } else {
+    if (tid < k) xbl = xb_in[(long long)gi * k + tid];
+  }
+
+  int bi[NBL], bj[NBL];
+  block_of_lane<KP, NT>(tid, bi, bj);
+  double acc[NBL][16];
+  double b1acc;
+  int ptot;
+  assemble_point<KP, kBigChunk, ASSEMBLED, NT>(sm.u.ch, trees, c, gi, tid, nbr_cnt, nbr_idx,
+                                               pt, col_off, yo_in, yb_in, bi, bj, acc, b1acc,
+                                               ptot);
+  if (tid == 0) sm.ptot = ptot;  // counted by wave 0
+  __syncthreads();
+  ptot = sm.ptot;
+  if (ptot == 0) {  // no accepted observation: var left unchanged (:220, :226)
+    if (tid == 0 && info) info[gi] = make_int2(0, 0);
+    if constexpr (ASSEMBLED) {
+      if (tid < k) xa_out[(long long)gi * k + tid] = xbl;
+    }
+    return;
+  }
+
+  const double inflat_r8 = (double)c.inflat;
+#pragma unroll
+  for (int it = 0; it < NBL; ++it) {
+    if (tid + NT * it < NBLK && bi[it] == bj[it]) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ii = 4 * bi[it] + r;
+        acc[it][5 * r] = ii < k ? acc[it][5 * r] + inflat_r8 : 1.0;
+      }
+    }
+  }
+  if (tid < KP) {  // padding of T: decoupled unit rows
+    sm.tq[tid][0] = 1.0;
+    sm.tq[tid][1] = 0.0;
+    sm.tau[tid] = 0.0;
+  }
+  if (tid == 0) sm.tq[KP][1] = 0.0;
+  const double xb_mean = (double)(seq_sum_f32(xbl) * c.nmember_inv);  // fp32 (:671)
+  double ux = (tid < k) ? (double)xbl - xb_mean : 0.0;                 // x', then Q^T x'
+  double ub = (tid < KP) ? b1acc : 0.0;                                // Yb d, then Q^T b1
+
+  auto ld4 = [](const double *p, double (&o)[4]) {
+    const double2 a0 = *reinterpret_cast<const double2 *>(p);
+    const double2 a1 = *reinterpret_cast<const double2 *>(p + 2);
+    o[0] = a0.x; o[1] = a0.y; o[2] = a1.x; o[3] = a1.y;
+  };
+  // column j of the lower block triangle -> dst (4 rows per block of block column j/4)
+#define CWBL_PUBLISH(jj, dst)                                                                \
+  do {                                                                                     \
+    const int J_ = (jj) >> 2, q_ = (jj) & 3;                                               \
+    _Pragma("unroll") for (int it = 0; it < NBL; ++it) {                                   \
+      if (tid + NT * it < NBLK && bj[it] == J_) {                                          \
+        double cv[4];                                                                      \
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                    \
+          const double a0 = acc[it][4 * r], a1 = acc[it][4 * r + 1];                       \
+          const double a2 = acc[it][4 * r + 2], a3 = acc[it][4 * r + 3];                   \
+          cv[r] = q_ == 0 ? a0 : q_ == 1 ? a1 : q_ == 2 ? a2 : a3;                         \
+        }                                                                                  \
+        *reinterpret_cast<double2 *>(&(dst)[4 * bi[it]]) = make_double2(cv[0], cv[1]);     \
+        *reinterpret_cast<double2 *>(&(dst)[4 * bi[it] + 2]) = make_double2(cv[2], cv[3]); \
+      }                                                                                    \
+    }                                                                                      \
+  } while (0)
+
+  // ---- Householder tridiagonalisation ----------------------------------------------------
+  double trace = 0.0;
+  for (int j = 0; j < k; ++j) {
+    const int J = j >> 2, qj = j & 3;
+    __syncthreads();  // previous step's readers of col are done
+    CWBL_PUBLISH(j, sm.col);
+    __syncthreads();
+    const double dj = sm.col[j];
+    trace += dj;
+    if (tid == 0) sm.tq[j][0] = dj;
+    if (j >= k - 2) {  // trailing 2x2 block: already tridiagonal
+      if (j == k - 2 && tid == 0) sm.tq[j + 1][1] = sm.col[j + 1];
+      continue;
+    }
+    const double x = (tid > j + 1 && tid < k) ? sm.col[tid] : 0.0;
+    const double alpha = sm.col[j + 1];
+    double xn2 = x * x, z1 = 0.0, z2 = 0.0, z3 = 0.0;
+    bsum4(xn2, z1, z2, z3);
+    double tau = 0.0, beta = alpha, scal = 0.0;
+    if (xn2 > 0.0) {  // dlarfg, fp64 rcp/rsq refined to ~1 ulp
+      const double a2 = fma(alpha, alpha, xn2);
+      beta = -copysign(a2 * rsq64(a2), alpha);
+      tau = (beta - alpha) * rcp64(beta);
+      scal = rcp64(alpha - beta);
+    }
+    if (tid == 0) {
+      sm.tq[j + 1][1] = beta;
+      sm.tau[j] = tau;
+    }
+    if (tau == 0.0) continue;  // H_j = I (uniform)
+    const double v = tid == j + 1 ? 1.0 : x * scal;
+    if (tid < KP) sm.vb[tid] = v;
+    __syncthreads();
+    double s1p = 0.0;
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) {
+      if (tid + NT * it < NBLK && bi[it] >= J) {
+        double vi[4], vj[4];
+        ld4(&sm.vb[4 * bi[it]], vi);
+        ld4(&sm.vb[4 * bj[it]], vj);
+        double pr[4], pc[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pr[r] = acc[it][4 * r] * vj[0];
+#pragma unroll
+          for (int q = 1; q < 4; ++q) pr[r] = fma(acc[it][4 * r + q], vj[q], pr[r]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pc[q] = acc[it][q] * vi[0];
+#pragma unroll
+          for (int r = 1; r < 4; ++r) pc[q] = fma(acc[it][4 * r + q], vi[r], pc[q]);
+        }
+        double sp = vi[0] * pr[0];
+#pragma unroll
+        for (int r = 1; r < 4; ++r) sp = fma(vi[r], pr[r], sp);
+        double *dst = &sm.u.pb[bi[it]][4 * bj[it]];
+        *reinterpret_cast<double2 *>(dst) = make_double2(pr[0], pr[1]);
+        *reinterpret_cast<double2 *>(dst + 2) = make_double2(pr[2], pr[3]);
+        if (bi[it] != bj[it]) {
+          if (bj[it] >= J) {
+            double *dt = &sm.u.pb[bj[it]][4 * bi[it]];
+            *reinterpret_cast<double2 *>(dt) = make_double2(pc[0], pc[1]);
+            *reinterpret_cast<double2 *>(dt + 2) = make_double2(pc[2], pc[3]);
+          }
+          sp = sp + sp;
+        }
+        s1p += sp;
+      }
+    }
+    double s2 = v * ux, s3 = v * ub, s1 = s1p, z4 = 0.0;
+    bsum4(s2, s3, s1, z4);  // also publishes pb (barrier inside)
+    s1 *= tau;              // p . v with p = tau A v
+    ux = fma(-tau * s2, v, ux);
+    ub = fma(-tau * s3, v, ub);
+    double pp = 0.0;
+    if (tid < KP && tid > j) {
+      const double *prow = &sm.u.pb[tid >> 2][tid & 3];
+#pragma unroll
+      for (int cb = 0; cb < SM::NB; ++cb) pp += prow[4 * cb];
+    }
+    const double p = (tid > j && tid < k) ? tau * pp : 0.0;
+    const double w = fma(-0.5 * tau * s1, v, p);
+    if (tid < KP) sm.wb[tid] = w;
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) {
+      if (tid + NT * it < NBLK && bi[it] >= J) {
+        double vi[4], vj[4], wi[4], wj[4];
+        ld4(&sm.vb[4 * bi[it]], vi);
+        ld4(&sm.vb[4 * bj[it]], vj);
+        ld4(&sm.wb[4 * bi[it]], wi);
+        ld4(&sm.wb[4 * bj[it]], wj);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            acc[it][4 * r + q] = fma(-vi[r], wj[q], fma(-wi[r], vj[q], acc[it][4 * r + q]));
+        if (bj[it] == J) {  // keep v_j in the entries of column j the steps no longer read
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const bool keep = 4 * bi[it] + r > j + 1;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              acc[it][4 * r + q] = (keep && q == qj) ? vi[r] : acc[it][4 * r + q];
+          }
+        }
+      }
+    }
+  }
+  if (tid < KP) {
+    sm.tq[tid][2] = ub;
+    sm.tq[tid][3] = ux;
+  }
+  __syncthreads();
+
+  // ---- T^-1/2 u2 by quadrature (wave 0), u1^T T^-1 u2 exactly ----------------------------
+  const double m = inflat_r8;
+  const double ratio = trace / m - (double)(k - 1);
+  int level = 1;
+  double dec = 10.0;
+  while (level < kQuadLevels && dec < ratio) {
+    dec *= 10.0;
+    ++level;
+  }
+  if (wave == 0) {
+    const int node = lane & 31, side = lane >> 5;
+    double sigma = 0.0, omega = 0.0;
+    if (node < kQuadNodes) {
+      const double2 tw = c.quad[(level - 1) * 32 + node];
+      sigma = m * tw.x;
+      omega = sqrt(m) * tw.y;
+    }
+    const int dir = side ? -4 : 4;
+    const double *q = &sm.tq[side ? KP - 1 : 0][0];
+    const int cs = side ? 5 : 1;  // coupling with the previous mirrored row
+    // one row of the forward elimination (identical in both passes)
+    auto fwd = [&](int t, double &dl, double &gt) {
+      const double *qt = q + dir * t;
+      const double ct = qt[cs];
+      const double l = ct * rcp64(dl);
+      dl = fma(-l, ct, qt[0] + sigma);
+      gt = fma(-l, gt, qt[3]);
+    };
+    constexpr int S = 8, NS = H / S;
+    double ckd[NS], ckg[NS];
+    double dl = q[0] + sigma, gt = q[3];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      ckd[s] = dl;
+      ckg[s] = gt;
+#pragma unroll
+      for (int t = S * s + 1; t < S * s + S; ++t) fwd(t, dl, gt);
+      if (s + 1 < NS) fwd(S * s + S, dl, gt);
+    }
+    // meeting rows H-1 (top) and H (bottom)
+    const double cm = sm.tq[H][1];
+    const double dlo = __shfl_xor(dl, 32, 64), go = __shfl_xor(gt, 32, 64);
+    double xv = (gt * dlo - cm * go) / fma(dl, dlo, -cm * cm);
+    double *ym = sm.Ym + side * H, *zm = sm.Zm + side * H;
+    for (int s = NS - 1; s >= 0; --s) {  // recompute the segment, then substitute back
+      double hh[S], mmv[S];
+      double d2 = ckd[s], g2 = ckg[s];
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        const int t = S * s + i;
+        if (i > 0) fwd(t, d2, g2);
+        const double rd = rcp64(d2);
+        hh[i] = g2 * rd;
+        mmv[i] = (t + 1 < H) ? q[dir * (t + 1) + cs] * rd : 0.0;  // c_{t+1} / dl_t
+      }
+#pragma unroll
+      for (int i = S - 1; i >= 0; --i) {
+        const int t = S * s + i;
+        if (t != H - 1) xv = fma(-mmv[i], xv, hh[i]);
+        const double ys = half_sum_dpp(omega * xv);
+        if (node == 0) ym[t] = ys;
+        if (node == 31) zm[t] = xv;
+      }
+    }
+  }
+  __syncthreads();
+  const int wi = tid < H ? tid : H + (KP - 1 - tid);
+  const double zl = tid < KP ? sm.Zm[wi] : 0.0;
+  double yl = tid < KP ? sm.Ym[wi] : 0.0;
+  double dsum = tid < KP ? sm.tq[tid][2] * zl : 0.0, z5 = 0.0, z6 = 0.0, z7 = 0.0;
+  bsum4(dsum, z5, z6, z7);
+  const double d = dsum;  // wbar . x' = u1 . T^-1 u2
+
+  // ---- back-transform y <- Q y, two reflectors per reduction -----------------------------
+  auto vrow = [&](const double *src, int j) {
+    return tid == j + 1 ? 1.0 : (tid > j + 1 && tid < k) ? src[tid] : 0.0;
+  };
+  int j = k - 3;
+  for (; j >= 1; j -= 2) {
+    __syncthreads();  // readers of col/col2 (previous pair) are done
+    CWBL_PUBLISH(j, sm.col);
+    CWBL_PUBLISH(j - 1, sm.col2);
+    __syncthreads();
+    const double t1 = sm.tau[j], t0 = sm.tau[j - 1];
+    const double v1 = t1 == 0.0 ? 0.0 : vrow(sm.col, j);
+    const double v0 = t0 == 0.0 ? 0.0 : vrow(sm.col2, j - 1);
+    double a1 = v1 * yl, b0 = v0 * yl, c01 = v0 * v1, z8 = 0.0;
+    bsum4(a1, b0, c01, z8);
+    yl = fma(-t1 * a1, v1, yl);
+    yl = fma(-t0 * fma(-t1 * a1, c01, b0), v0, yl);
+  }
+  if (j == 0) {
+    __syncthreads();
+    CWBL_PUBLISH(0, sm.col);
+    __syncthreads();
+    const double t0 = sm.tau[0];
+    const double v0 = t0 == 0.0 ? 0.0 : vrow(sm.col, 0);
+    double a0 = v0 * yl, z9 = 0.0, z10 = 0.0, z11 = 0.0;
+    bsum4(a0, z9, z10, z11);
+    yl = fma(-t0 * a0, v0, yl);
+  }
+  const double sk = sqrt((double)(k - 1));
+  float xal = tid < KP ? (float)(xb_mean + (d + sk * yl)) : 0.0f;
+
+  // ---- RTPP / RTPS (:684-698), fp32 in the reference's order -------------------------
+  if (c.use_rtpp || c.use_rtps) {
+    const float xa_mean = seq_sum_f32(xal) * c.nmember_inv;
+    const double xpl = tid < k ? (double)xbl - xb_mean : 0.0;
+    float xap = 0.0f;
+    if (tid < k) {
+      xap = xal - xa_mean;
+      if (c.use_rtpp)
+        xap = (float)((double)((1.0f - c.rtpp_alpha) * xap) + (double)c.rtpp_alpha * xpl);
+    }
+    if (c.use_rtps) {
+      const float xb_std = (float)seq_sumsq_f64(xpl);
+      const float xa_std = seq_sum_f32(xap * xap);
+      xap = xap * (c.rtps_alpha * sqrtf(xb_std / xa_std) - c.rtps_alpha + 1.0f);
+    }
+    xal = xa_mean + xap;
+  }
+
+  if (tid < k) {
+    if constexpr (ASSEMBLED) xa_out[(long long)gi * k + tid] = xal;
+    else slab.var[P + slab.L * tid] = xal;
+  }
+  if (tid == 0 && info) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
+}
+#undef CWBL_PUBLISH
+
+template <int KP>
+static hipError_t launch_big_kp(hipStream_t s, bool assembled, const TreeDesc *trees,
+                                SolveConsts c, SlabDev slab, long long g0, int npts,
+                                const int *nbr_cnt, const int *nbr_idx,
+                                const long long *col_off, const float *yo, const float *yb,
+                                const float *xb, float *xa, int2 *info) {
+  if (assembled)
+    hipLaunchKernelGGL((solve_tq_big_kernel<KP, true>), dim3(npts), dim3(kBigThreads), 0, s,
+                       trees, c, slab, g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa,
+                       info);
+  else
+    hipLaunchKernelGGL((solve_tq_big_kernel<KP, false>), dim3(npts), dim3(kBigThreads), 0, s,
+                       trees, c, slab, g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa,
+                       info);
+  return hipGetLastError();
+}
+
+hipError_t launch_solve_tq_big(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,
+                               SolveConsts c, SlabDev slab, long long g0, int npts,
+                               const int *nbr_cnt, const int *nbr_idx,
+                               const long long *col_off, const float *yo, const float *yb,
+                               const float *xb, float *xa, int2 *info) {
+  if (npts <= 0) return hipSuccess;
+  if (c.quad == nullptr) return hipErrorInvalidValue;
+  switch (kp) {
+    case 96:
+      return launch_big_kp<96>(s, assembled, trees, c, slab, g0, npts, nbr_cnt, nbr_idx,
+                               col_off, yo, yb, xb, xa, info);
+    case 128:
+      return launch_big_kp<128>(s, assembled, trees, c, slab, g0, npts, nbr_cnt, nbr_idx,
+                                col_off, yo, yb, xb, xa, info);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace cwbl

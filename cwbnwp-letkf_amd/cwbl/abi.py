@@ -14,7 +14,7 @@ ABI_VERSION = 1
 MAX_NVAR = 5
 NUM_GTS_TYPES = 29
 NUM_RADAR_TYPES = 4
-MAX_MEMBERS = 64
+MAX_MEMBERS = 128
 
 GTS_SOUND, GTS_SYNOP, GTS_GPSPW, GTS_METAR, GTS_SHIPS = 1, 2, 8, 10, 11
 RADAR_DBZ, RADAR_VR, RADAR_ZDR, RADAR_KDP = 1, 2, 3, 4

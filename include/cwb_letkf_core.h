@@ -51,7 +51,7 @@ extern "C" {
 #define CWBL_MAX_NVAR        5   /* obs variables per GTS report (u,v,t,p,q) */
 #define CWBL_NUM_GTS_TYPES  29   /* module_param.f90:172 num_gts_indexes     */
 #define CWBL_NUM_RADAR_TYPES 4   /* module_param.f90:212 num_radar_indexes   */
-#define CWBL_MAX_MEMBERS    64   /* k supported by the v1 solve kernels      */
+#define CWBL_MAX_MEMBERS    128  /* largest k the solve kernels support      */
 
 /* GTS type ids (module_param.f90:143-171); only these five are assimilated
  * (module_localization.f90:59-72). */

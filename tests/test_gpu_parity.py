@@ -57,7 +57,7 @@ def test_solve_batch_matches_reference(k):
     assert worst_eig <= EIG_TOL, worst_eig
 
 
-@pytest.mark.parametrize("k", [8, 40, 64])
+@pytest.mark.parametrize("k", [8, 40, 64, 128])
 def test_solve_batch_tq_matches_reference(k):
     """Without an eigenvalue output cwbl_solve_batch runs the tridiagonalisation + quadrature
     kernel (cwbl_tq.hip): same increments as the reference's dsyevd path."""
@@ -75,10 +75,19 @@ def test_solve_batch_tq_matches_reference(k):
     assert worst <= INCR_TOL, worst
 
 
-def test_k128_reports_unsupported():
+def test_k_limits():
+    """k up to 128 is supported (k > 64 on the 256-thread kernel); beyond that, and the
+    eigenvalue output above k = 64 (the Jacobi path), report UNSUPPORTED."""
     with pytest.raises(abi.CwblError, match="UNSUPPORTED"):
-        abi.Core(128, device=0)
+        abi.Core(129, device=0)
     _cores.clear()
+    c = core(128)
+    g = golden("solve_k128.npz")
+    col = g["col_off"]
+    off = np.array([0, col[1] - col[0]], np.int64)
+    with pytest.raises(abi.CwblError, match="UNSUPPORTED"):
+        c.solve_batch(off, g["yo"][col[0]:col[1]], g["yb"][:col[1] * 128], g["xb"][0][None],
+                      inflat_of(128, g["multi_infl"][0]), 1, 0.95, 1, 0.95, want_evals=True)
 
 
 SEARCHES = ["search_3d.npz", "search_3d_overflow.npz", "search_2d.npz",
@@ -275,6 +284,31 @@ def test_dense_radar_c5_block_vs_oracle():
     ref = sub(w.var).copy()
     ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
     rc = oracle().orc_analyze_var(w.k, 0, norain, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(sub(w.x), sub(w.y), sub(w.alt), ref)),
+                                  16, C.byref(abi.Stats()))
+    assert rc == 0
+    rel = increment_rel_rms(sub(var), ref, sub(w.var))
+    assert rel <= INCR_TOL, rel
+
+
+@pytest.mark.parametrize("k", [80, 128])
+def test_large_ensemble_block_vs_oracle(k):
+    """configs[3]-shaped large ensembles (k = 128, and k = 80 on the KP = 96 kernel) on a
+    30x30x50 cut of the C2 grid: GPU vs the oracle on a 6x6-column block."""
+    import ctypes as C
+    from cwbl import synth
+    w = synth.make("c4", scale=0.1, k=k)
+    c = core(w.k)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    var = w.var.copy()
+    st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+    assert np.isfinite(var).all()
+    assert st.nonconverged == 0
+    j0, i0, nb = 12, 12, 6
+    sub = lambda a: np.ascontiguousarray(a[..., j0:j0 + nb, i0:i0 + nb])  # noqa: E731
+    ref = sub(w.var).copy()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
                                   C.byref(abi.make_slab(sub(w.x), sub(w.y), sub(w.alt), ref)),
                                   16, C.byref(abi.Stats()))
     assert rc == 0
