@@ -143,11 +143,16 @@ def main():
         ms_search = sum(s.ms_search for s in stats)
         flops = synth.flops_total(k, solved, nobs_sum)
         achieved = flops / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else 0.0
-        traffic = None
+        kp = ((k + 7) // 8) * 8 if k <= 64 else (96 if k <= 96 else 128)
+        kname = ("solve_kernel" if jacobi else
+                 "solve_tq_kernel" if kp <= 64 else "solve_tq_big_kernel") + f"<{kp}, false>"
+        traffic = None  # HBM bytes per launch from the committed PMC pass of this kernel
         pmc = os.path.join(REPO, "profiles", "pmc_solve_traffic.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                pm = json.load(f)
+            if pm.get("kernel", "").endswith(kname) and args.config == pm.get("config", "c2"):
+                traffic = pm.get("hbm_bytes_per_launch")
         out = {
             "metric": METRIC,
             "value": pts_total / elapsed,
@@ -178,7 +183,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK_TFLOPS,
                 "traffic": traffic,
-                "kernel": f"{'solve_kernel' if jacobi else 'solve_tq_kernel'}<{((k + 7) // 8) * 8},false>",
+                "kernel": kname,
                 "note": "FP64 flops F(k,p) of SURVEY.md 8(d) per solve launch / HIP-event launch time (rank 0)",
             },
             "detail": {
