@@ -307,6 +307,7 @@ SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps,
   if (const char *e = std::getenv("CWBL_DEBUG_MAX_SWEEPS")) c.max_sweeps = std::atoi(e);
   c.quad = S.quad.as<double2>();
   if (const char *e = std::getenv("CWBL_DEBUG_TQ_STOP")) c.debug_stop = std::atoi(e);
+  if (const char *e = std::getenv("CWBL_DEBUG_STAGGER")) c.stagger = std::atoi(e);
   return c;
 }
 

@@ -234,10 +234,12 @@ __device__ __forceinline__ float slot_r2(const f32x4 d, int dim, float q0, float
 // the Yb Yb^T (dsyrk) and Yb d products of letkf_solve (:598-700), in fp64.
 // Lane L owns the 4x4 blocks L, L+64, ... of the lower block triangle (bi >= bj).
 // ---------------------------------------------------------------------------------------
-template <int KP, int CHUNK>
+// Staged columns: E = float (converted by the consumer) or double (converted once here;
+// products of the fp32 values stay exact in fp64 either way).
+template <int KP, int CHUNK, class E = float>
 struct ColumnChunk {
-  float yb[CHUNK][KP];
-  float yo[CHUNK];
+  E yb[CHUNK][KP];
+  E yo[CHUNK];
   unsigned long long expt[32];  // expf table (kExpT) in LDS: per-lane lookups stay on chip
 };
 
@@ -252,9 +254,9 @@ struct AsmLayout {
 // yo = omm * error_inv, in the reference's fp32 order; rejected columns as zeros) and calls
 // accumulate(nsl) on each staged chunk.  NT threads per point (`lane` = thread index).
 // Returns the number of accepted columns (p); with NT > 64 the count is valid in wave 0.
-template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64, class Acc>
+template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64, class E = float, class Acc>
 __device__ __forceinline__ int stage_columns(
-    ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
+    ColumnChunk<KP, CHUNK, E> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
     const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in, Acc &&accumulate) {
@@ -275,12 +277,12 @@ __device__ __forceinline__ int stage_columns(
       // column (its bg row is zero and its weight 0), which adds exact zeros to every sum.
       // So every gather of a chunk depends only on the neighbour slots: one round trip to
       // memory per chunk, with the next chunk's slots prefetched behind it.  Threads s,
-      // s + 32, s + 64, ... stage column s of the chunk, a part of its bg row each.
-      static_assert(CHUNK == 32, "32 staged columns per round");
-      constexpr int LPC = NT / 32;                       // threads per staged column
-      constexpr int V4 = KP / 4, VH = V4 / LPC;          // float4 per bg row, per thread
-      static_assert(V4 % LPC == 0, "bg row split");
-      const int sl = lane & 31, half = lane >> 5;
+      // s + CHUNK, s + 2 CHUNK, ... stage column s of the chunk, a part of its bg row each.
+      static_assert(NT % CHUNK == 0 && CHUNK <= 64, "threads per staged column");
+      constexpr int LPC = NT / CHUNK;                    // threads per staged column
+      constexpr int VH = KP / (2 * LPC);                 // float2 of the bg row per thread
+      static_assert(KP % (2 * LPC) == 0, "bg row split");
+      const int sl = lane % CHUNK, half = lane / CHUNK;
       const int *__restrict__ lst = nbr_idx + lbase;
       int slot_next = 0;
       if (sl < min(CHUNK, npairs)) slot_next = gld(lst, (unsigned)(sl / nvar * kListLanes));
@@ -294,17 +296,22 @@ __device__ __forceinline__ int stage_columns(
         uint8_t okb = 0;
         float err = 1.0f, omm = 0.0f;
         f32x4 rd = {0.0f, 0.0f, 0.0f, 0.0f};
-        f32x4 g[VH];
+        float2 g[VH];
 #pragma unroll
-        for (int i = 0; i < VH; ++i) g[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int i = 0; i < VH; ++i) g[i] = make_float2(0.0f, 0.0f);
         if (live) {
           okb = gld(T.col_ok, (unsigned)col);
           err = gld(T.col_err, (unsigned)col);
           omm = gld(T.col_omm, (unsigned)col);
           rd = gld4(reinterpret_cast<const float *>(T.rdata), 4u * (unsigned)slot);
-          const unsigned b0 = (unsigned)(col * KP + 4 * VH * half);
+          const unsigned b0 = (unsigned)(col * KP + 2 * VH * half);
+          typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-          for (int i = 0; i < VH; ++i) g[i] = gld4(T.col_bg, b0 + 4u * i);
+          for (int i = 0; i < VH; ++i) {
+            const char *bp = reinterpret_cast<const char *>(T.col_bg) + (unsigned)((b0 + 2u * i) * 4u);
+            const f32x2 t = *gptr(reinterpret_cast<const f32x2 *>(bp));
+            g[i] = make_float2(t.x, t.y);
+          }
         }
         // prefetch the next chunk's slots behind this chunk's gathers
         const int nb = base + CHUNK;
@@ -317,13 +324,16 @@ __device__ __forceinline__ int stage_columns(
           yo = omm * w;  // omm * error_inv (:451)
         }
         ptot += __popcll(__ballot(ok && half == 0));  // counted by wave 0
-        if (half == 0) ch.yo[sl] = yo;
-        float *dst = &ch.yb[sl][4 * VH * half];
+        if (half == 0) ch.yo[sl] = (E)yo;
+        E *dst = &ch.yb[sl][2 * VH * half];
 #pragma unroll
         for (int i = 0; i < VH; ++i) {
-          float4 y;  // bg * error_inv (:452)
-          y.x = g[i].x * w; y.y = g[i].y * w; y.z = g[i].z * w; y.w = g[i].w * w;
-          *reinterpret_cast<float4 *>(dst + 4 * i) = y;
+          const float y0 = g[i].x * w, y1 = g[i].y * w;  // bg * error_inv (:452)
+          if constexpr (sizeof(E) == 8) {
+            *reinterpret_cast<double2 *>(dst + 2 * i) = make_double2((double)y0, (double)y1);
+          } else {
+            *reinterpret_cast<float2 *>(dst + 2 * i) = make_float2(y0, y1);
+          }
         }
         __syncthreads();
         accumulate(nsl);
@@ -335,10 +345,10 @@ __device__ __forceinline__ int stage_columns(
     const int ncol = (int)(c1 - c0);
     for (int base = 0; base < ncol; base += CHUNK) {
       const int nsl = min(CHUNK, ncol - base);
-      if (lane < nsl) ch.yo[lane] = yo_in[c0 + base + lane];
+      if (lane < nsl) ch.yo[lane] = (E)yo_in[c0 + base + lane];
       for (int e = lane; e < nsl * KP; e += NT) {
         const int s = e / KP, m = e - s * KP;
-        ch.yb[s][m] = m < k ? yb_in[(c0 + base + s) * k + m] : 0.0f;
+        ch.yb[s][m] = m < k ? (E)yb_in[(c0 + base + s) * k + m] : (E)0.0f;
       }
       __syncthreads();
       accumulate(nsl);
@@ -351,9 +361,9 @@ __device__ __forceinline__ int stage_columns(
 
 // Column assembly on the VALU: thread L accumulates the 4x4 blocks L, L+NT, ... of the lower
 // block triangle of Yb Yb^T, and threads < KP the entries of Yb d.
-template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64>
+template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64, class E = float>
 __device__ __forceinline__ void assemble_point(
-    ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
+    ColumnChunk<KP, CHUNK, E> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
     const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in,
@@ -365,16 +375,26 @@ __device__ __forceinline__ void assemble_point(
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[it][e] = 0.0;
   b1acc = 0.0;
-  ptot = stage_columns<KP, CHUNK, ASSEMBLED, NT>(
+  ptot = stage_columns<KP, CHUNK, ASSEMBLED, NT, E>(
       ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in, [&](int nsl) {
         for (int s = 0; s < nsl; ++s) {
 #pragma unroll
           for (int it = 0; it < NBL; ++it) {
             if (lane + NT * it < NBLK) {
-              const float4 ra = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bi[it]]);
-              const float4 rb = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bj[it]]);
-              const double a4[4] = {ra.x, ra.y, ra.z, ra.w};
-              const double b4[4] = {rb.x, rb.y, rb.z, rb.w};
+              double a4[4], b4[4];
+              if constexpr (sizeof(E) == 8) {
+                const double2 a0 = *reinterpret_cast<const double2 *>(&ch.yb[s][4 * bi[it]]);
+                const double2 a1 = *reinterpret_cast<const double2 *>(&ch.yb[s][4 * bi[it] + 2]);
+                const double2 c0 = *reinterpret_cast<const double2 *>(&ch.yb[s][4 * bj[it]]);
+                const double2 c1 = *reinterpret_cast<const double2 *>(&ch.yb[s][4 * bj[it] + 2]);
+                a4[0] = a0.x; a4[1] = a0.y; a4[2] = a1.x; a4[3] = a1.y;
+                b4[0] = c0.x; b4[1] = c0.y; b4[2] = c1.x; b4[3] = c1.y;
+              } else {
+                const float4 ra = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bi[it]]);
+                const float4 rb = *reinterpret_cast<const float4 *>(&ch.yb[s][4 * bj[it]]);
+                a4[0] = ra.x; a4[1] = ra.y; a4[2] = ra.z; a4[3] = ra.w;
+                b4[0] = rb.x; b4[1] = rb.y; b4[2] = rb.z; b4[3] = rb.w;
+              }
 #pragma unroll
               for (int r = 0; r < 4; ++r)
 #pragma unroll

@@ -68,6 +68,7 @@ struct SolveConsts {
   float r2;                   // gc1999**2
   int   max_sweeps;           // Jacobi sweep cap (CWBL_DEBUG_MAX_SWEEPS overrides; ablation only)
   const double2 *quad;        // [kQuadLevels][32] (t2, w) of the x^-1/2 rule (solve_tq_kernel)
+  int   stagger;              // CWBL_DEBUG_STAGGER: start-phase offset unit in cycles (experiment)
   int   debug_stop;           // CWBL_DEBUG_TQ_STOP: 1 = after assembly, 2 = after
                               // tridiagonalisation, 3 = after quadrature (timing ablation only)
 };

@@ -28,9 +28,18 @@
 // 1e-13 up to M/m = 1e8), well inside the parity tolerance.
 #include "cwbl_device.h"
 
+#include <type_traits>
+
 namespace cwbl {
 
-constexpr int kTqChunk = 32;  // columns staged per round
+// Assembly of Yb Yb^T: fp64 FMAs on the lower 4x4 blocks from columns staged in LDS as
+// fp64 (16 per round), or on the matrix cores (v_mfma_f64_16x16x4 on 16x16 tiles of
+// [Yb; yo], 32 float columns per round).  On gfx950 the FP64 matrix and vector rates are
+// equal and the two do not co-issue; the tiles waste 44% of their products at KP = 40, so
+// the block form is faster.  The MFMA form is kept for comparison (kTqMfmaAssembly).
+constexpr bool kTqMfmaAssembly = true;
+constexpr int kTqChunk = kTqMfmaAssembly ? 32 : 16;  // columns staged per round
+using TqStage = std::conditional_t<kTqMfmaAssembly, float, double>;
 
 // LDS of one point (KP = 40: 9.4 KB, so 16 waves fit a CU).  The big union is reused by
 // phase: staged columns -> half of A -> {Householder vectors + A v partials}, then
@@ -55,7 +64,7 @@ struct TqSmem {
   static constexpr int REG = cap();
   static constexpr int pb_base(int J) { return REG - (NB - J) * PLD; }
   union {
-    ColumnChunk<KP, kTqChunk> ch;
+    ColumnChunk<KP, kTqChunk, TqStage> ch;
     double ah[KP / 2][KP + 2];            // half of A on its way from MFMA tiles to blocks
     double reg[REG];                      // hv[0, NHV) | y after the loop | pb
   } u;
@@ -92,6 +101,10 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   if (gi >= npts) return;
   const int lane = threadIdx.x;
   const int k = c.k;
+  if (c.stagger > 0 && blockIdx.x < 4096) {  // experiment: offset the first waves' phases
+    const int slot = (int)(blockIdx.x >> 8) >> 2;  // 0..3 for the 16 first-round slots of a CU
+    for (int t = 0; t < slot * c.stagger / 8000; ++t) __builtin_amdgcn_s_sleep(125);
+  }
 
   long long P = 0;  // var index of member 0
   float3 pt = make_float3(0.0f, 0.0f, 0.0f);  // the point's projected x, y and altitude
@@ -109,65 +122,79 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     if (lane < k) xbl = xb_in[(long long)gi * k + lane];
   }
 
-  f64x4 tile[MfmaLayout<KP>::NTL];
-  double b1acc;
-  int ptot;
-  assemble_point_mfma<KP, kTqChunk, ASSEMBLED>(sm.u.ch, trees, c, gi, lane, nbr_cnt, nbr_idx,
-                                               pt, col_off, yo_in, yb_in, tile, b1acc,
-                                               ptot);
-
-  if (ptot == 0) {  // no accepted observation: var left unchanged (:220, :226)
-    if (lane == 0 && info) info[gi] = make_int2(0, 0);
-    if constexpr (ASSEMBLED) {
-      if (lane < k) xa_out[(long long)gi * k + lane] = xbl;
-    }
-    return;
-  }
-
-  if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the rest
-    double t = b1acc;
-#pragma unroll
-    for (int q = 0; q < MfmaLayout<KP>::NTL; ++q) t += tile[q][0] + tile[q][3];
-    if (lane == 0 && info) info[gi] = make_int2(ptot, (int)t);
-    return;
-  }
-  // ---- A = inflat*I + Yb Yb^T: MFMA tiles -> LDS (two row halves) -> 4x4 register blocks --
   int bi[NBL], bj[NBL];
   block_of_lane<KP>(lane, bi, bj);
   double acc[NBL][16];
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    int t = 0;
-#pragma unroll
-    for (int I = 0; I < MfmaLayout<KP>::NT; ++I)
-#pragma unroll
-      for (int J = 0; J <= I; ++J, ++t) {
-        const int col = 16 * J + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * I + (lane >> 4) + 4 * r;
-          if (row / H == half && row < KP && col < KP) sm.u.ah[row - half * H][col] = tile[t][r];
-          if (MfmaLayout<KP>::YO_ROW && half == 0 && row == KP && col < KP)
-            sm.wb[col] = tile[t][r];  // row KP of Y' Y'^T = Yb d
-        }
+  double b1acc;
+  int ptot;
+  if constexpr (!kTqMfmaAssembly) {
+    assemble_point<KP, kTqChunk, ASSEMBLED, 64, TqStage>(sm.u.ch, trees, c, gi, lane, nbr_cnt,
+                                                         nbr_idx, pt, col_off, yo_in, yb_in,
+                                                         bi, bj, acc, b1acc, ptot);
+    if (ptot == 0) {  // no accepted observation: var left unchanged (:220, :226)
+      if (lane == 0 && info) info[gi] = make_int2(0, 0);
+      if constexpr (ASSEMBLED) {
+        if (lane < k) xa_out[(long long)gi * k + lane] = xbl;
       }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < NBL; ++it) {
-      if (lane + 64 * it < NBLK && (4 * bi[it]) / H == half) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const double *src = &sm.u.ah[4 * bi[it] + r - half * H][4 * bj[it]];
-          const double2 x0 = *reinterpret_cast<const double2 *>(src);
-          const double2 x1 = *reinterpret_cast<const double2 *>(src + 2);
-          acc[it][4 * r] = x0.x; acc[it][4 * r + 1] = x0.y;
-          acc[it][4 * r + 2] = x1.x; acc[it][4 * r + 3] = x1.y;
-        }
-      }
+      return;
     }
-    __syncthreads();
+    if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the rest
+      if (lane == 0 && info) info[gi] = make_int2(ptot, (int)(acc[0][0] + b1acc));
+      return;
+    }
+  } else {
+    f64x4 tile[MfmaLayout<KP>::NTL];
+    assemble_point_mfma<KP, kTqChunk, ASSEMBLED>(sm.u.ch, trees, c, gi, lane, nbr_cnt, nbr_idx,
+                                                 pt, col_off, yo_in, yb_in, tile, b1acc, ptot);
+    if (ptot == 0) {
+      if (lane == 0 && info) info[gi] = make_int2(0, 0);
+      if constexpr (ASSEMBLED) {
+        if (lane < k) xa_out[(long long)gi * k + lane] = xbl;
+      }
+      return;
+    }
+    if (c.debug_stop == 1) {
+      double t = b1acc;
+#pragma unroll
+      for (int q = 0; q < MfmaLayout<KP>::NTL; ++q) t += tile[q][0] + tile[q][3];
+      if (lane == 0 && info) info[gi] = make_int2(ptot, (int)t);
+      return;
+    }
+    // MFMA tiles -> LDS (two row halves) -> 4x4 register blocks
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      int t = 0;
+#pragma unroll
+      for (int I = 0; I < MfmaLayout<KP>::NT; ++I)
+#pragma unroll
+        for (int J = 0; J <= I; ++J, ++t) {
+          const int col = 16 * J + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * I + (lane >> 4) + 4 * r;
+            if (row / H == half && row < KP && col < KP) sm.u.ah[row - half * H][col] = tile[t][r];
+            if (MfmaLayout<KP>::YO_ROW && half == 0 && row == KP && col < KP)
+              sm.wb[col] = tile[t][r];  // row KP of Y' Y'^T = Yb d
+          }
+        }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < NBL; ++it) {
+        if (lane + 64 * it < NBLK && (4 * bi[it]) / H == half) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double *src = &sm.u.ah[4 * bi[it] + r - half * H][4 * bj[it]];
+            const double2 x0 = *reinterpret_cast<const double2 *>(src);
+            const double2 x1 = *reinterpret_cast<const double2 *>(src + 2);
+            acc[it][4 * r] = x0.x; acc[it][4 * r + 1] = x0.y;
+            acc[it][4 * r + 2] = x1.x; acc[it][4 * r + 3] = x1.y;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (MfmaLayout<KP>::YO_ROW && lane < KP) b1acc = sm.wb[lane];
   }
-  if (MfmaLayout<KP>::YO_ROW && lane < KP) b1acc = sm.wb[lane];
   const double inflat_r8 = (double)c.inflat;
 #pragma unroll
   for (int it = 0; it < NBL; ++it) {
