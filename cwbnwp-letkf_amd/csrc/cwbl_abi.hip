@@ -78,7 +78,7 @@ struct ObsType {
 // cwbl_analyze_var calls of one obs set; the column tables are rebuilt per call (they
 // depend on the variable's QC parameters).
 struct TreeBufs {
-  int entry = -1, dim = 0;
+  int entry = -1, dim = 0, depth = 0;
   float hinv = 0.0f, vinv = 0.0f;
   DevBuf nodes, rdata, ind, col_bg, col_omm, col_err, col_ok;
   HostTree host;
@@ -170,7 +170,7 @@ int require_device() {
 // Builds the trees of one family (build_tree, module_localization.f90:35-167) and their
 // column tables.  Appends TreeDesc entries.
 int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &descs,
-                 int &list_cap) {
+                 int &list_cap, int &max_depth) {
   struct Pending { int entry; int type_id; const cwbl_type_params *tp; float hinv, vinv; };
   std::vector<Pending> pend;
   const int ntypes = family == 0 ? CWBL_NUM_GTS_TYPES : CWBL_NUM_RADAR_TYPES;
@@ -212,7 +212,8 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
       auto nt = std::make_unique<TreeBufs>();
       nt->entry = pd.entry; nt->dim = tdim; nt->hinv = pd.hinv; nt->vinv = pd.vinv;
       build_kdtree(nx.data(), n, tdim, nt->host);
-      if (tree_depth(nt->host) >= kSearchStackDepth)
+      nt->depth = tree_depth(nt->host);
+      if (nt->depth >= kSearchStackDepth)
         return fail(CWBL_ERR_UNSUPPORTED, "k-d tree too deep (%d obs)", n);
       const HostTree &h = nt->host;
       HIPCHK(nt->nodes.ensure(h.nodes.size() * sizeof(TreeNode)));
@@ -262,7 +263,8 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
     d.max_lz = tp->max_lz_pts;
     d.list_off = list_cap;
     d.q1_undef = q1u;
-    list_cap += tp->max_lz_pts;
+    list_cap += list_span(tp->max_lz_pts);
+    max_depth = std::max(max_depth, tb->depth);
     descs.push_back(d);
   }
   return CWBL_OK;
@@ -455,8 +457,9 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   // ---- trees (cached per obs set) + column tables ------------------------------------------
   std::vector<TreeDesc> descs;
   int list_cap = 0;
-  if (int rc = build_family(0, vp, descs, list_cap)) return rc;
-  if (int rc = build_family(1, vp, descs, list_cap)) return rc;
+  int max_depth = 1;
+  if (int rc = build_family(0, vp, descs, list_cap, max_depth)) return rc;
+  if (int rc = build_family(1, vp, descs, list_cap, max_depth)) return rc;
   const int nt = (int)descs.size();
   st.ntrees = nt;
   if (nt == 0 || npts == 0) {  // `if(all(.not. succeed)) cycle` (:66)
@@ -518,7 +521,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     hipEvent_t a, b, cc;
     HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b)); HIPCHK(event(ev + 2, &cc));
     HIPCHK(hipEventRecord(a, S.stream));
-    HIPCHK(launch_search(S.stream, dtrees, nt, list_cap, c.r2, sd, g0, nb,
+    HIPCHK(launch_search(S.stream, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb,
                          S.nbr_cnt.as<int>(), S.nbr_idx.as<int>(), nullptr, dst));
     HIPCHK(hipEventRecord(b, S.stream));
     if (S.kp > kMaxWaveKP)
@@ -636,7 +639,8 @@ int cwbl_search(int nobs, const float *obs_xyz, float hclr, float vclr, int max_
   }
   TreeBufs tb;
   build_kdtree(nx.data(), nobs, dim3 ? 3 : 2, tb.host);
-  if (tree_depth(tb.host) >= kSearchStackDepth)
+  tb.depth = tree_depth(tb.host);
+  if (tb.depth >= kSearchStackDepth)
     return fail(CWBL_ERR_UNSUPPORTED, "k-d tree too deep");
   const HostTree &h = tb.host;
   HIPCHK(tb.nodes.ensure(std::max<size_t>(h.nodes.size(), 1) * sizeof(TreeNode)));
@@ -668,7 +672,8 @@ int cwbl_search(int nobs, const float *obs_xyz, float hclr, float vclr, int max_
   HIPCHK(S.qnf.ensure((size_t)nq * 4));
   HIPCHK(S.qidx.ensure((size_t)nq * max_lz_pts * 4));
   HIPCHK(S.qr2.ensure((size_t)nq * max_lz_pts * 4));
-  HIPCHK(launch_search_single(S.stream, dd.as<TreeDesc>(), search_r2(), nq, S.qxyz.as<float>(),
+  HIPCHK(launch_search_single(S.stream, dd.as<TreeDesc>(), tb.depth, search_r2(), nq,
+                              S.qxyz.as<float>(),
                               max_lz_pts, S.qnf.as<int>(), S.qidx.as<int>(), S.qr2.as<float>()));
   HIPCHK(hipMemcpyAsync(nfound, S.qnf.p, (size_t)nq * 4, hipMemcpyDeviceToHost, S.stream));
   HIPCHK(hipMemcpyAsync(idx, S.qidx.p, (size_t)nq * max_lz_pts * 4, hipMemcpyDeviceToHost,

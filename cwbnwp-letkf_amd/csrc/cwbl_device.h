@@ -285,7 +285,7 @@ __device__ __forceinline__ int stage_columns(
       const int sl = lane % CHUNK, half = lane / CHUNK;
       const int *__restrict__ lst = nbr_idx + lbase;
       int slot_next = 0;
-      if (sl < min(CHUNK, npairs)) slot_next = gld(lst, (unsigned)(sl / nvar * kListLanes));
+      if (sl < min(CHUNK, npairs)) slot_next = gld(lst, list_slot(sl / nvar));
       for (int base = 0; base < npairs; base += CHUNK) {
         const int nsl = min(CHUNK, npairs - base);
         const bool live = sl < nsl;
@@ -316,7 +316,7 @@ __device__ __forceinline__ int stage_columns(
         // prefetch the next chunk's slots behind this chunk's gathers
         const int nb = base + CHUNK;
         if (sl < min(CHUNK, npairs - nb))
-          slot_next = gld(lst, (unsigned)((nb + sl) / nvar * kListLanes));
+          slot_next = gld(lst, list_slot((nb + sl) / nvar));
         const bool ok = live && okb != 0;
         float w = 0.0f, yo = 0.0f;
         if (ok) {

@@ -100,9 +100,10 @@ hipError_t launch_obs_prep(hipStream_t s, int k, int kp, int family, int type_id
                            const int is_assim[5], float norain, const int *slot_obs,
                            float *col_bg, float *col_omm, float *col_err, uint8_t *col_ok);
 
-hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int list_cap,
-                         float r2, SlabDev slab, long long g0, int npts, int *nbr_cnt,
-                         int *nbr_idx, float *nbr_r2, DevStats *stats);
+// depth: the deepest tree's level count (tree_depth), which sizes the traversal stacks
+hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int depth,
+                         int list_cap, float r2, SlabDev slab, long long g0, int npts,
+                         int *nbr_cnt, int *nbr_idx, float *nbr_r2, DevStats *stats);
 
 // nbr_idx holds tree slots (search with nbr_r2 = nullptr); the solve recomputes r2
 hipError_t launch_solve_neighbors(hipStream_t s, int kp, const TreeDesc *trees,
@@ -128,22 +129,31 @@ hipError_t launch_solve_tq_big(hipStream_t s, int kp, bool assembled, const Tree
                                const long long *col_off, const float *yo, const float *yb,
                                const float *xb, float *xa, int2 *info);
 
-hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, float r2, int nq,
-                                const float *q_xyz, int max_lz, int *nfound, int *idx,
+hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, int depth, float r2,
+                                int nq, const float *q_xyz, int max_lz, int *nfound, int *idx,
                                 float *r2out);
 
 hipError_t launch_reduce_info(hipStream_t s, const int2 *info, int n, DevStats *stats);
 
 constexpr int kSearchStackDepth = 40;  // max k-d tree depth the search kernel supports
 
-// Neighbour lists of the analysis path are interleaved by groups of kListLanes points:
-// slot s of point g lives at list_index(g, cap, off) + s * kListLanes.  Lanes of one search
-// wave then write their lists side by side (whole cache lines) instead of 64 scattered
-// streams.  Buffers hold round_up(npts, kListLanes) * cap entries.
+// Neighbour lists of the analysis path are interleaved by groups of kListLanes points and
+// kListGroup slots: slot s of point g lives at list_index(g, cap, off) + list_slot(s).  A
+// search wave then stores 16 B per lane side by side (whole cache lines) instead of 64
+// scattered 4-B streams, and a solve reading 32 consecutive slots of one point touches 8
+// lines instead of 32.  cap and off are multiples of kListGroup (list_span); buffers hold
+// round_up(npts, kListLanes) * cap entries.
 constexpr int kListLanes = 64;
+constexpr int kListGroup = 4;
+__host__ __device__ inline int list_span(int max_lz) {
+  return (max_lz + kListGroup - 1) / kListGroup * kListGroup;
+}
 __host__ __device__ inline long long list_index(long long g, int cap, int off) {
   return (g / kListLanes) * (long long)cap * kListLanes + (long long)off * kListLanes +
-         (g % kListLanes);
+         (g % kListLanes) * kListGroup;
+}
+__host__ __device__ inline unsigned list_slot(int s) {
+  return (unsigned)(s / kListGroup) * (kListGroup * kListLanes) + (unsigned)(s % kListGroup);
 }
 
 int supported_kp(int k);      // smallest compiled KP >= k, or -1

@@ -131,30 +131,52 @@ __device__ int search_tree(const TreeDesc &T, float q0, float q1, float q2, floa
   const int dim = T.tree_dim;
   int count = 0, sp = 0, node = 0;
   overflow = false;
+  // analysis lists: slots are buffered kListGroup at a time and stored as one 16-B write
+  static_assert(kListGroup == 4, "int4 groups");
+  int4 grp = make_int4(0, 0, 0, 0);
+  auto flush = [&]() {
+    if (!out_r2 && (count % kListGroup) != 0)
+      *reinterpret_cast<int4 *>(out_idx + list_slot(count - count % kListGroup)) = grp;
+  };
   while (true) {
     const TreeNode nd = nodes[node];
     if (nd.cut_dim < 0) {  // process_terminal_node_fixedball (:1654-1707)
-      for (int i = nd.l; i <= nd.u; ++i) {
-        const float4 d = T.rdata[i];
-        const float dx = d.x - q0, dy = d.y - q1;
-        float sd = dx * dx;
-        sd = sd + dy * dy;
-        if (dim == 3) {
-          const float dz = d.z - q2;
-          sd = sd + dz * dz;
-        }
-        if (sd <= r2) {
-          if (count == T.max_lz) { overflow = true; return count; }
-          if (out_r2) {  // cwbl_search: original obs index and distance
-            out_idx[count] = T.ind[i];
-            out_r2[count] = sd;
-          } else {       // analysis: the tree slot (columns are stored in slot order)
-            out_idx[(long long)count * kListLanes] = i;
+      // the bucket's points are loaded four at a time ahead of the tests, so one round
+      // trip to memory covers four candidates; tests and appends stay in index order
+      for (int i0 = nd.l; i0 <= nd.u; i0 += 4) {
+        float4 d[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          d[e] = T.rdata[min(i0 + e, nd.u)];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = i0 + e;
+          const float dx = d[e].x - q0, dy = d[e].y - q1;
+          float sd = dx * dx;
+          sd = sd + dy * dy;
+          if (dim == 3) {
+            const float dz = d[e].z - q2;
+            sd = sd + dz * dz;
           }
-          ++count;
+          if (i <= nd.u && sd <= r2) {
+            if (count == T.max_lz) { overflow = true; flush(); return count; }
+            if (out_r2) {  // cwbl_search: original obs index and distance
+              out_idx[count] = T.ind[i];
+              out_r2[count] = sd;
+            } else {       // analysis: the tree slot (columns are stored in slot order)
+              const int g = count % kListGroup;
+              grp.x = g == 0 ? i : grp.x;
+              grp.y = g == 1 ? i : grp.y;
+              grp.z = g == 2 ? i : grp.z;
+              grp.w = i;
+              if (g == kListGroup - 1)
+                *reinterpret_cast<int4 *>(out_idx + list_slot(count - g)) = grp;
+            }
+            ++count;
+          }
         }
       }
-      if (sp == 0) return count;
+      if (sp == 0) { flush(); return count; }
       node = stk[--sp * 64];
       continue;
     }
@@ -213,7 +235,9 @@ __global__ void __launch_bounds__(64)
 search_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, float r2, Q qs,
               int npts, int *__restrict__ nbr_cnt, int *__restrict__ nbr_idx,
               float *__restrict__ nbr_r2, DevStats *stats) {
-  __shared__ int stk[kStackDepth * 64];
+  // traversal stacks, one column per lane; sized by the host to the deepest tree, so a
+  // shallow tree leaves LDS for more resident waves (the search is latency bound)
+  extern __shared__ int stk[];
   const int gi = blockIdx.x * 64 + threadIdx.x;
   if (gi >= npts) return;
   float px, py, pz;
@@ -239,22 +263,28 @@ search_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, floa
   if (trunc && stats) atomicAdd(&stats->lz_truncated, (unsigned long long)trunc);
 }
 
-hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int list_cap,
-                         float r2, SlabDev slab, long long g0, int npts, int *nbr_cnt,
-                         int *nbr_idx, float *nbr_r2, DevStats *stats) {
+static size_t stack_bytes(int depth) {
+  return (size_t)std::min(std::max(depth, 1), kStackDepth) * 64 * sizeof(int);
+}
+
+hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int depth,
+                         int list_cap, float r2, SlabDev slab, long long g0, int npts,
+                         int *nbr_cnt, int *nbr_idx, float *nbr_r2, DevStats *stats) {
   if (npts <= 0) return hipSuccess;
   SlabQuery q{slab, g0};
-  hipLaunchKernelGGL(search_kernel<SlabQuery>, dim3((npts + 63) / 64), dim3(64), 0, s, trees,
+  hipLaunchKernelGGL(search_kernel<SlabQuery>, dim3((npts + 63) / 64), dim3(64),
+                     stack_bytes(depth), s, trees,
                      ntrees, list_cap, r2, q, npts, nbr_cnt, nbr_idx, nbr_r2, stats);
   return hipGetLastError();
 }
 
-hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, float r2, int nq,
-                                const float *q_xyz, int max_lz, int *nfound, int *idx,
+hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, int depth, float r2,
+                                int nq, const float *q_xyz, int max_lz, int *nfound, int *idx,
                                 float *r2out) {
   if (nq <= 0) return hipSuccess;
   ListQuery q{q_xyz};
-  hipLaunchKernelGGL(search_kernel<ListQuery>, dim3((nq + 63) / 64), dim3(64), 0, s, tree, 1,
+  hipLaunchKernelGGL(search_kernel<ListQuery>, dim3((nq + 63) / 64), dim3(64),
+                     stack_bytes(depth), s, tree, 1,
                      max_lz, r2, q, nq, nfound, idx, r2out, (DevStats *)nullptr);
   return hipGetLastError();
 }
