@@ -125,6 +125,7 @@ __device__ __forceinline__ float dis2_from_bnd(float x, float amin, float amax) 
 // with an explicit stack: because the ball never shrinks in the fixed-ball search, the
 // decision to visit the farther child can be taken before descending the closer one, and
 // LIFO order then reproduces the recursive visiting order exactly.
+constexpr int kAhead = 4;  // bucket points loaded ahead of their tests
 __device__ int search_tree(const TreeDesc &T, float q0, float q1, float q2, float r2,
                            int *out_idx, float *out_r2, int *stk, bool &overflow) {
   const TreeNode *__restrict__ nodes = T.nodes;
@@ -143,13 +144,13 @@ __device__ int search_tree(const TreeDesc &T, float q0, float q1, float q2, floa
     if (nd.cut_dim < 0) {  // process_terminal_node_fixedball (:1654-1707)
       // the bucket's points are loaded four at a time ahead of the tests, so one round
       // trip to memory covers four candidates; tests and appends stay in index order
-      for (int i0 = nd.l; i0 <= nd.u; i0 += 4) {
-        float4 d[4];
+      for (int i0 = nd.l; i0 <= nd.u; i0 += kAhead) {
+        float4 d[kAhead];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < kAhead; ++e)
           d[e] = T.rdata[min(i0 + e, nd.u)];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < kAhead; ++e) {
           const int i = i0 + e;
           const float dx = d[e].x - q0, dy = d[e].y - q1;
           float sd = dx * dx;
