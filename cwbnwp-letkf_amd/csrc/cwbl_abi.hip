@@ -541,6 +541,15 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     solve_ev.push_back({ev + 1, ev + 2});
     ev += 3;
   }
+  if (vp->tune_q) {  // letkf_driver's Q species post-step (:253-278), on the resident slab
+    hipEvent_t a, b;
+    HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b));
+    HIPCHK(hipEventRecord(a, S.stream));
+    HIPCHK(launch_tune_q(S.stream, sd, S.k));
+    HIPCHK(hipEventRecord(b, S.stream));
+    solve_ev.push_back({ev, ev + 1});
+    ev += 2;
+  }
   hipEvent_t e_end;
   HIPCHK(event(ev, &e_end));
   if (sl->memory != CWBL_MEM_DEVICE)

@@ -100,6 +100,9 @@ hipError_t launch_obs_prep(hipStream_t s, int k, int kp, int family, int type_id
                            const int is_assim[5], float norain, const int *slot_obs,
                            float *col_bg, float *col_omm, float *col_err, uint8_t *col_ok);
 
+// letkf_tune_q over the analysed region of s.var (module_letkf_core.f90:702-733)
+hipError_t launch_tune_q(hipStream_t st, SlabDev s, int k);
+
 // depth: the deepest tree's level count (tree_depth), which sizes the traversal stacks
 hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int depth,
                          int list_cap, float r2, SlabDev slab, long long g0, int npts,

@@ -290,6 +290,41 @@ hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, int depth, 
   return hipGetLastError();
 }
 
+// letkf_tune_q (module_letkf_core.f90:702-733) over the analysed region of var(nx,ny,nz,0:k-1),
+// one thread per point.  Both member sums run in member order in fp32 (`sum(var)` and
+// `sum(var, mask=var>0)`, :720); a point with no positive member gets ratio = 0/0 (or x/0),
+// so its non-negative members become NaN (Q3, replicated).  HBM bound: 2 reads + 1 write of
+// the k values, coalesced across threads (neighbouring points are adjacent in memory).
+__global__ void __launch_bounds__(256)
+tune_q_kernel(SlabDev s, int k, long long npts) {
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= npts) return;
+  const int i = (int)(g % s.ix_lim);
+  const long long r = g / s.ix_lim;
+  const int j = (int)(r % s.iy_lim);
+  const int kz = (int)(r / s.iy_lim);
+  float *__restrict__ v = s.var + i + (long long)s.nx * (j + (long long)s.ny * kz);
+  float sum = 0.0f, sum_pos = 0.0f;
+  for (int m = 0; m < k; ++m) {
+    const float x = v[m * s.L];
+    sum = sum + x;
+    if (x > 0.0f) sum_pos = sum_pos + x;
+  }
+  const float ratio = sum / sum_pos;
+  for (int m = 0; m < k; ++m) {
+    const float x = v[m * s.L];
+    v[m * s.L] = x < 0.0f ? 0.0f : ratio * x;  // where (var < 0) 0 elsewhere ratio*var
+  }
+}
+
+hipError_t launch_tune_q(hipStream_t st, SlabDev s, int k) {
+  const long long npts = (long long)s.ix_lim * s.iy_lim * s.nz;
+  if (npts <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tune_q_kernel, dim3((unsigned)((npts + 255) / 256)), dim3(256), 0, st, s,
+                     k, npts);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------
 // solve_kernel<KP>: one wavefront (64 lanes) per grid point, members padded to KP
 // ---------------------------------------------------------------------------------------

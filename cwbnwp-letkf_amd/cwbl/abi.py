@@ -10,7 +10,7 @@ import os
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_NVAR = 5
 NUM_GTS_TYPES = 29
 NUM_RADAR_TYPES = 4
@@ -59,7 +59,7 @@ class TypeParams(C.Structure):
 
 class VarParams(C.Structure):
     _fields_ = [("multi_infl", C.c_float), ("use_rtpp", C.c_int), ("rtpp_alpha", C.c_float),
-                ("use_rtps", C.c_int), ("rtps_alpha", C.c_float), ("reserved", C.c_int),
+                ("use_rtps", C.c_int), ("rtps_alpha", C.c_float), ("tune_q", C.c_int),
                 ("gts", TypeParams * NUM_GTS_TYPES), ("radar", TypeParams * NUM_RADAR_TYPES)]
 
 
@@ -161,11 +161,13 @@ def type_params(use_it=1, max_lz_pts=500, hclr=-1.0, vclr=-1.0, err_muti=1.0, er
 
 
 def var_params(multi_infl=1.0, use_rtpp=0, rtpp_alpha=0.85, use_rtps=0, rtps_alpha=0.85,
-               gts=None, radar=None):
-    """inflation_nml defaults (module_config.f90:312-317); gts/radar: {type_id: TypeParams}."""
+               gts=None, radar=None, tune_q=0):
+    """inflation_nml defaults (module_config.f90:312-317); gts/radar: {type_id: TypeParams};
+    tune_q=1 for the Q species (letkf_tune_q after the analysis, module_letkf_core.f90:253-278)."""
     vp = VarParams()
     vp.multi_infl, vp.use_rtpp, vp.rtpp_alpha = multi_infl, int(use_rtpp), rtpp_alpha
     vp.use_rtps, vp.rtps_alpha = int(use_rtps), rtps_alpha
+    vp.tune_q = int(tune_q)
     for i in range(NUM_GTS_TYPES):
         vp.gts[i] = type_params(use_it=0)
     for i in range(NUM_RADAR_TYPES):

@@ -62,7 +62,7 @@ program abi_case_driver
     end do
     close(10)
 
-    if (cwbl_abi_version() /= 1) stop "ABI version mismatch"
+    if (cwbl_abi_version() /= 2) stop "ABI version mismatch"
     ip = cwbl_init_params(k, 0, wf, norain, CWBL_Q1_REPLICATE, 0, 0_c_size_t)
     call cwbl_check(cwbl_init(ip), 'cwbl_init')
     os = cwbl_obs_set(ng, nr, c_loc(g), c_loc(r), CWBL_MEM_HOST, 0)

@@ -51,7 +51,7 @@ module letkf_core_gpu
         real(c_float)          :: rtpp_alpha
         integer(c_int)         :: use_rtps
         real(c_float)          :: rtps_alpha
-        integer(c_int)         :: reserved
+        integer(c_int)         :: tune_q       ! 1: letkf_tune_q after the analysis
         type(cwbl_type_params) :: gts(CWBL_NUM_GTS_TYPES)
         type(cwbl_type_params) :: radar(CWBL_NUM_RADAR_TYPES)
     end type cwbl_var_params

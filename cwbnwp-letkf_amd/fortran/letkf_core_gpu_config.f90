@@ -37,7 +37,14 @@ contains
         vp%rtpp_alpha = RTPP_Alpha(ivar)
         vp%use_rtps   = merge(1, 0, use_RTPS(ivar))
         vp%rtps_alpha = RTPS_Alpha(ivar)
-        vp%reserved   = 0
+        ! letkf_driver tunes the hydrometeor species after the loop (:253-278)
+        select case (trim(var_update(ivar)))
+        case ('QVAPOR', 'QRAIN', 'QSNOW', 'QGRAUP', 'QHAIL', 'QNRAIN', 'QNSNOW', &
+              'QNGRAUPEL', 'QNHAIL')
+            vp%tune_q = 1
+        case default
+            vp%tune_q = 0
+        end select
         do i = 1, CWBL_NUM_GTS_TYPES
             call off(vp%gts(i))
         end do

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CWBL_ABI_VERSION 1
+#define CWBL_ABI_VERSION 2
 
 #define CWBL_MAX_NVAR        5   /* obs variables per GTS report (u,v,t,p,q) */
 #define CWBL_NUM_GTS_TYPES  29   /* module_param.f90:172 num_gts_indexes     */
@@ -141,7 +141,9 @@ typedef struct cwbl_var_params {
   float rtpp_alpha;
   int   use_rtps;
   float rtps_alpha;
-  int   reserved;
+  int   tune_q;          /* 1: letkf_tune_q (module_letkf_core.f90:702-733) on the analysed
+                          * region after the analysis, as letkf_driver does for the Q
+                          * species (QVAPOR ... QNHAIL, :253-278); Q3 (0/0 = NaN) replicated */
   cwbl_type_params gts[CWBL_NUM_GTS_TYPES];     /* index = gts type id - 1 */
   cwbl_type_params radar[CWBL_NUM_RADAR_TYPES]; /* index = radar type id - 1 */
 } cwbl_var_params;
@@ -177,7 +179,7 @@ typedef struct cwbl_stats {
   double    ms_total;        /* wall time of the call */
   double    ms_prep;         /* tree build + obs QC tables */
   double    ms_search;       /* neighbour search kernels */
-  double    ms_solve;        /* solve kernels */
+  double    ms_solve;        /* solve kernels (+ the tune_q pass when requested) */
   double    ms_copy;         /* host<->device copies of the slab (host memory only) */
 } cwbl_stats;
 

@@ -12,6 +12,9 @@ Fixtures
   G2 search_*.npz          build_tree/get_lz KATs on kdtree2 (module_localization.f90, module_kdtree2.f90)
   G3 gc.npz                Gaspari_Cohn_1999 (module_localization.f90:333-364)
   G4 driver_*.npz          one variable through the driver loop (module_letkf_core.f90:59-240)
+  G5 tune_q.npz            letkf_tune_q KATs (module_letkf_core.f90:702-733), incl. Q3 columns
+
+`python oracle/gen_goldens.py tuneq` regenerates only G5 (and updates its manifest entry).
 """
 import json
 import os
@@ -216,6 +219,50 @@ def T(family, type_id, nobs, hclr, vclr, max_lz, err_muti=1.0, err_rej=5.0, is_a
     return d
 
 
+# ------------------------------------------------------------------------------------- G5
+def gen_tuneq(seed):
+    """q(nx,ny,nz,k) fields: mixed signs, all-zero columns (Q3: 0/0 -> NaN), all-negative
+    columns (x/0 -> -inf, zeros -> NaN), all-positive columns, tiny and large magnitudes."""
+    rng = np.random.default_rng(seed)
+    cases = []
+    for k, (nx, ny, nz) in ((8, (7, 5, 3)), (40, (6, 4, 2)), (128, (3, 3, 2))):
+        q = rng.normal(0.0, 1.0, (nx, ny, nz, k)).astype(f4) * f4(1e-3)
+        q[0, 0, 0, :] = 0.0                                   # Q3: all zero
+        q[1, 0, 0, :] = -np.abs(q[1, 0, 0, :])                # no positive member
+        q[1, 0, 0, 0] = 0.0
+        q[2, 0, 0, :] = np.abs(q[2, 0, 0, :]) + f4(1e-4)      # all positive (ratio 1-ish)
+        q[0, 1, 0, :] = q[0, 1, 0, :] * f4(1e-30)             # tiny
+        q[1, 1, 0, :] = q[1, 1, 0, :] * f4(1e6)               # large
+        q[2, 1, 0, ::3] = 0.0                                 # exact zeros mixed in
+        if nz > 1:
+            q[0, 0, 1, :] = np.where(np.arange(k) == k - 1, f4(5e-4), f4(-1e-4))  # one positive
+        out = np.frombuffer(run("tuneq", b(np.array([k, nx, ny, nz], i4), q)), f4)
+        cases.append((k, q, out.reshape((nx, ny, nz, k), order="F").copy()))
+    d = {}
+    for i, (k, q, o) in enumerate(cases):
+        d[f"k{i}"] = np.int32(k)
+        d[f"q_in{i}"] = q
+        d[f"q_out{i}"] = o
+    d["ncases"] = np.int32(len(cases))
+    return d
+
+
+def main_tuneq():
+    d = gen_tuneq(501)
+    np.savez_compressed(os.path.join(OUT, "tune_q.npz"), **d)
+    mpath = os.path.join(OUT, "MANIFEST.json")
+    with open(mpath) as f:
+        manifest = json.load(f)
+    manifest["files"]["tune_q.npz"] = {
+        "what": "G5 letkf_tune_q KAT (source text of module_letkf_core.f90:702-733 with the "
+                "cpu(myid)%loc_nx/loc_ny bounds replaced by size(q,1)/size(q,2))",
+        "seed": 501, "ks": [int(d[f"k{i}"]) for i in range(int(d["ncases"]))],
+        "nan_out": int(sum(np.isnan(d[f"q_out{i}"]).sum() for i in range(int(d["ncases"]))))}
+    with open(mpath, "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+    print(json.dumps(manifest["files"]["tune_q.npz"], indent=1))
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build oracle/_ref/ref_harness first (make -C oracle ref)")
@@ -305,4 +352,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["tuneq"]:
+        main_tuneq()
+    else:
+        main()
+        main_tuneq()

@@ -6,6 +6,7 @@
 #   module_param.f90, module_config.f90, module_eigen.f90, module_kdtree2.f90
 # and the source text of
 #   letkf_solve        (module_letkf_core.f90:598-700)
+#   letkf_tune_q       (module_letkf_core.f90:702-733)
 #   Gaspari_Cohn_1999  (module_localization.f90:333-364)
 # cut out at build time into a wrapper module (their home modules cannot be compiled here:
 # module_letkf_core/module_localization `use` grid/gts_omboma/radar, whose chain needs the
@@ -42,11 +43,19 @@ done
   echo "    implicit none"
   echo "contains"
   awk '/^    function letkf_solve\(/,/end function letkf_solve/' "$REF/module_letkf_core.f90"
+  # letkf_tune_q's loop bounds read the MPI decomposition (cpu(myid)%loc_nx/loc_ny, from
+  # module_mpi_util, which cannot be compiled here).  The harness passes q allocated as
+  # (loc_nx, loc_ny, nz, k), as letkf_driver does for the mass-grid Q species (:85), so
+  # the bounds are replaced by size(q,1) / size(q,2); the body is otherwise unchanged.
+  awk '/^    subroutine letkf_tune_q\(/,/end subroutine letkf_tune_q/' "$REF/module_letkf_core.f90" \
+    | sed -e 's/cpu(myid) *% *loc_ny/size(q, 2)/' -e 's/cpu(myid) *% *loc_nx/size(q, 1)/'
   awk '/pure function Gaspari_Cohn_1999\(/,/end function Gaspari_Cohn_1999/' "$REF/module_localization.f90"
   echo "end module ref_extract"
 } > "$TMP/ref_extract.f90"
 grep -q "end function letkf_solve" "$TMP/ref_extract.f90"
 grep -q "end function Gaspari_Cohn_1999" "$TMP/ref_extract.f90"
+grep -q "end subroutine letkf_tune_q" "$TMP/ref_extract.f90"
+if grep -q "cpu(myid)" "$TMP/ref_extract.f90"; then echo "build_ref: tune_q bounds not replaced"; exit 1; fi
 $CPP "$TMP/ref_extract.f90" > "$TMP/ref_extract.F90"
 
 cd "$TMP"

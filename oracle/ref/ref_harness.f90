@@ -3,12 +3,13 @@
 ! TEST INFRASTRUCTURE ONLY (built by oracle/ref/build_ref.sh into oracle/_ref/).
 ! Real reference code exercised: module param / config (read_namelist) / eigen
 ! (set_optimal_workspace_for_eigen, inverse_matrix, sqrt_matrix) / kdtree2_module
-! (kdtree2_create, kdtree2_r_nearest) and the source text of letkf_solve and
+! (kdtree2_create, kdtree2_r_nearest) and the source text of letkf_solve, letkf_tune_q and
 ! Gaspari_Cohn_1999.  The glue that the reference keeps in modules we cannot compile here
 ! (build_tree/get_lz normalisation, letkf_yoyb, the driver loop) is restated below,
 ! line for line, with the file:line it follows.
 !
-! Usage: ref_harness <mode> <in.bin> <out.bin>, modes: consts | solve | search | gc | driver
+! Usage: ref_harness <mode> <in.bin> <out.bin>,
+! modes: consts | solve | search | gc | driver | tuneq
 ! All files are unformatted stream (little-endian int32 / real32 / real64).
 module harness_lib
     use param
@@ -176,6 +177,22 @@ contains
         close(21)
     end subroutine do_gc
 
+    ! letkf_tune_q KATs.  in: k nx ny nz (i4), q(nx,ny,nz,k) (r4).  out: q after the call
+    subroutine do_tuneq
+        integer :: k, nx, ny, nz
+        real, allocatable :: q(:,:,:,:)
+        open(40, file=trim(fin), access='stream', form='unformatted', status='old')
+        read(40) k, nx, ny, nz
+        call setup_k(k)
+        allocate(q(nx, ny, nz, k))
+        read(40) q
+        close(40)
+        call letkf_tune_q(nz, q)
+        open(21, file=trim(fout), access='stream', form='unformatted', status='replace')
+        write(21) q
+        close(21)
+    end subroutine do_tuneq
+
     include 'ref_driver.inc'
 
 end module harness_lib
@@ -200,6 +217,8 @@ program ref_harness
         call do_gc
     case ('driver')
         call do_driver
+    case ('tuneq')
+        call do_tuneq
     case default
         stop "ref_harness: unknown mode"
     end select

@@ -314,3 +314,51 @@ def test_large_ensemble_block_vs_oracle(k):
     assert rc == 0
     rel = increment_rel_rms(sub(var), ref, sub(w.var))
     assert rel <= INCR_TOL, rel
+
+
+def test_tune_q_matches_reference():
+    """letkf_tune_q on the device (cwbl_var_params.tune_q) against the reference's compiled
+    letkf_tune_q (G5): bit for bit, including the Q3 NaN columns.  The single obs lies far
+    outside the domain, so the analysis leaves var untouched and only tune_q acts."""
+    g = golden("tune_q.npz")
+    for i in range(int(g["ncases"])):
+        k, q_in, q_out = int(g[f"k{i}"]), g[f"q_in{i}"], g[f"q_out{i}"]
+        nx, ny, nz, _ = q_in.shape
+        c = core(k)
+        b = abi.ObsSetBuilder()
+        far = np.array([[1e9, 1e9, 100.0]], np.float32)
+        b.add_radar(abi.RADAR_VR, far, np.zeros(1, np.float32), np.zeros((1, k), np.float32))
+        c.set_obs(b.build())
+        tp = abi.type_params(use_it=1, max_lz_pts=100, hclr=12.0, vclr=3.0, err_muti=1.0,
+                             err_rej=8.0)
+        vp = abi.var_params(radar={abi.RADAR_VR: tp}, tune_q=1)
+        var = np.ascontiguousarray(q_in.transpose(3, 2, 1, 0)).astype(np.float32)
+        x = np.tile(np.arange(nx, dtype=np.float32) * 2e3, (ny, 1))
+        y = np.tile((np.arange(ny, dtype=np.float32) * 2e3)[:, None], (1, nx))
+        alt = np.tile((np.arange(nz, dtype=np.float32) * 500.0)[:, None, None], (1, ny, nx))
+        slab = abi.make_slab(x, y, np.ascontiguousarray(alt), var)
+        st = c.analyze_var(vp, slab)
+        assert st.solved == 0 and st.ntrees == 1
+        got = var.transpose(3, 2, 1, 0)
+        np.testing.assert_array_equal(got.view(np.uint32), q_out.view(np.uint32))
+
+
+def test_driver_with_tune_q_vs_oracle():
+    """A Q-species variable: the analysis followed by tune_q, against the reference's
+    analysis (G4) with the oracle's tune_q applied (itself pinned bit-exact by G5)."""
+    import ctypes as C
+    case = DriverCase("driver_mixed.npz")
+    c = core(case.k, case.wf, case.norain)
+    c.set_obs(case.obs_set())
+    slab, var = case.slab()
+    vp = case.vp
+    vp.tune_q = 1
+    c.analyze_var(vp, slab)
+    vp.tune_q = 0
+    ref = np.ascontiguousarray(case.var_out, np.float32).copy()
+    k, nz, ny, nx = ref.shape
+    oracle().orc_tune_q(k, nx, ny, nz, case.ix_lim, case.iy_lim, ref.ctypes.data_as(C.c_void_p))
+    xb = np.ascontiguousarray(case.var_in, np.float32).copy()
+    oracle().orc_tune_q(k, nx, ny, nz, case.ix_lim, case.iy_lim, xb.ctypes.data_as(C.c_void_p))
+    rel = increment_rel_rms(var, ref, xb)
+    assert rel <= INCR_TOL, rel

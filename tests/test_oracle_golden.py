@@ -112,3 +112,19 @@ def test_driver_one_variable(name):
     else:
         assert increment_rel_rms(var, case.var_out, case.var_in) <= 1e-6
     assert st.solved > 0
+
+
+def tune_q_cases():
+    g = golden("tune_q.npz")
+    return [(int(g[f"k{i}"]), g[f"q_in{i}"], g[f"q_out{i}"]) for i in range(int(g["ncases"]))]
+
+
+def test_tune_q_bitexact():
+    """orc_tune_q against letkf_tune_q (module_letkf_core.f90:702-733) compiled from the
+    reference: bit for bit, including the Q3 NaN columns (0/0) and the all-negative ones."""
+    for k, q_in, q_out in tune_q_cases():
+        nx, ny, nz, _ = q_in.shape
+        var = np.asfortranarray(q_in.copy())
+        oracle().orc_tune_q(k, nx, ny, nz, nx, ny, var.ctypes.data)
+        np.testing.assert_array_equal(var.view(np.uint32), q_out.view(np.uint32))
+        assert np.isnan(q_out[0, 0, 0, :]).all()  # Q3 replicated by the reference itself
