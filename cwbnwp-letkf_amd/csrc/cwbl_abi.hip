@@ -630,6 +630,46 @@ int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const 
   return CWBL_OK;
 }
 
+int cwbl_pack_columns(const float *global, int nx, int ny, int nz, int px, int py,
+                      float *send) {
+  if (int rc = require_device()) return rc;
+  if (nx < 0 || ny < 0 || nz < 0 || px < 1 || py < 1 || px > kMaxRankDim || py > kMaxRankDim ||
+      (((long long)nx * ny * nz) > 0 && (!global || !send)))
+    return fail(CWBL_ERR_ARG, "cwbl_pack_columns: bad arguments");
+  Decomp d;
+  make_decomp(d, nx, ny, nz, px, py);
+  HIPCHK(launch_pack_columns(S.stream, global, d, send));
+  HIPCHK(hipStreamSynchronize(S.stream));
+  return CWBL_OK;
+}
+
+int cwbl_unpack_columns(const float *recv, int nx, int ny, int nz, int px, int py,
+                        float *global) {
+  if (int rc = require_device()) return rc;
+  if (nx < 0 || ny < 0 || nz < 0 || px < 1 || py < 1 || px > kMaxRankDim || py > kMaxRankDim ||
+      (((long long)nx * ny * nz) > 0 && (!global || !recv)))
+    return fail(CWBL_ERR_ARG, "cwbl_unpack_columns: bad arguments");
+  Decomp d;
+  make_decomp(d, nx, ny, nz, px, py);
+  HIPCHK(launch_unpack_columns(S.stream, recv, d, global));
+  HIPCHK(hipStreamSynchronize(S.stream));
+  return CWBL_OK;
+}
+
+int cwbl_vcoord_mean(const float *ph, long long n2d, int nz_ph, int k, int stagger, float g,
+                     float *alt) {
+  if (int rc = require_device()) return rc;
+  if (n2d < 0 || k < 1 || (stagger != 0 && stagger != 1) || nz_ph < (stagger == 0 ? 2 : 1) ||
+      (n2d > 0 && (!ph || !alt)))
+    return fail(CWBL_ERR_ARG, "cwbl_vcoord_mean: bad arguments");
+  // alpha = 1.0/(g*nmember) in default real (module_mpi_util.f90:496)
+  const float gk = g * (float)k;
+  const float alpha = 1.0f / gk;
+  HIPCHK(launch_vcoord_mean(S.stream, ph, n2d, nz_ph, k, stagger, alpha, alt));
+  HIPCHK(hipStreamSynchronize(S.stream));
+  return CWBL_OK;
+}
+
 int cwbl_search(int nobs, const float *obs_xyz, float hclr, float vclr, int max_lz_pts,
                 int nq, const float *q_xyz, int *nfound, int *idx, float *r2, int memory) {
   if (int rc = require_device()) return rc;

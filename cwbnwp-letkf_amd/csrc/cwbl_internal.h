@@ -100,6 +100,22 @@ hipError_t launch_obs_prep(hipStream_t s, int k, int kp, int family, int type_id
                            const int is_assim[5], float norain, const int *slot_obs,
                            float *col_bg, float *col_omm, float *col_err, uint8_t *col_ok);
 
+// Cyclic (block 1) column decomposition of letkf_local_info (module_mpi_util.f90:71-188) on a
+// px x py rank grid: rank r = id_x + id_y*px owns x = id_x + i*px, y = id_y + j*py.
+constexpr int kMaxRankDim = 64;
+struct Decomp {
+  int nx, ny, nz, px, py;
+  int cols_before[kMaxRankDim];  // columns owned by rank coordinates a < id_x
+  int rows_before[kMaxRankDim];  // rows owned by rank coordinates b < id_y
+};
+void make_decomp(Decomp &d, int nx, int ny, int nz, int px, int py);
+hipError_t launch_pack_columns(hipStream_t s, const float *global, const Decomp &d,
+                               float *send);
+hipError_t launch_unpack_columns(hipStream_t s, const float *recv, const Decomp &d,
+                                 float *global);
+hipError_t launch_vcoord_mean(hipStream_t s, const float *ph, long long n2d, int nz_ph, int k,
+                              int stagger, float alpha, float *alt);
+
 // letkf_tune_q over the analysed region of s.var (module_letkf_core.f90:702-733)
 hipError_t launch_tune_q(hipStream_t st, SlabDev s, int k);
 

@@ -1,0 +1,134 @@
+// cwbl_transpose.hip — device side of the member <-> column transposes around the core
+// (module_mpi_util.f90:71-358, 445-580).
+//
+// The reference moves each variable between "member layout" (rank m holds member m's whole
+// field, global(nx,ny,nz)) and "column layout" (every rank holds its cyclic columns for all
+// members, var(loc_nx,loc_ny,nz,0:k-1)) with mpi_alltoallv, packing and unpacking on the host.
+// Here the exchange is RCCL point-to-point over xGMI (cwbl/transpose.py); these kernels are
+// the packing on either side, done in HBM:
+//   pack_columns_kernel    letkf_scatter_grid send side (:224-258): global -> per-rank chunks
+//   unpack_columns_kernel  letkf_gather_grid receive side (:326-350): chunks -> global
+//   vcoord_mean_kernel     letkf_scatter_vcoord (:491-505): member mean of PH / g, destagger
+// All three are HBM bound byte moves (no arithmetic worth a matrix core): one thread per
+// element of the global field, so the global side is read or written fully coalesced and
+// the chunk side is px interleaved contiguous streams per wavefront.
+#include "../../include/cwb_letkf_core.h"
+#include "cwbl_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+namespace cwbl {
+
+namespace {
+
+// columns of a cyclic (block 1) split of n over p ranks owned by rank coordinate id
+__host__ __device__ inline int cyc_count(int n, int id, int p) {
+  return id < n ? (n - id + p - 1) / p : 0;
+}
+
+}  // namespace
+
+void make_decomp(Decomp &d, int nx, int ny, int nz, int px, int py) {
+  d.nx = nx; d.ny = ny; d.nz = nz; d.px = px; d.py = py;
+  int acc = 0;
+  for (int a = 0; a < px; ++a) { d.cols_before[a] = acc; acc += cyc_count(nx, a, px); }
+  acc = 0;
+  for (int b = 0; b < py; ++b) { d.rows_before[b] = acc; acc += cyc_count(ny, b, py); }
+}
+
+// element (x, y, z) of global(nx,ny,nz) -> its position in the rank-major chunk buffer
+__device__ inline long long chunk_pos(const Decomp &d, int x, int y, int z) {
+  const int idx = x % d.px, i = x / d.px;
+  const int idy = y % d.py, j = y / d.py;
+  const long long lnx = cyc_count(d.nx, idx, d.px), lny = cyc_count(d.ny, idy, d.py);
+  // ranks r' < r = idx + idy*px: whole rows of the rank grid, then this row's left part
+  const long long base = (long long)d.nz * ((long long)d.rows_before[idy] * d.nx +
+                                            lny * d.cols_before[idx]);
+  return base + i + lnx * (j + lny * z);
+}
+
+__global__ void __launch_bounds__(256)
+pack_columns_kernel(const float *__restrict__ global, Decomp d, float *__restrict__ send) {
+  const long long n = (long long)d.nx * d.ny * d.nz;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n;
+       e += (long long)gridDim.x * 256) {
+    const int x = (int)(e % d.nx);
+    const long long r = e / d.nx;
+    const int y = (int)(r % d.ny), z = (int)(r / d.ny);
+    send[chunk_pos(d, x, y, z)] = global[e];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+unpack_columns_kernel(const float *__restrict__ recv, Decomp d, float *__restrict__ global) {
+  const long long n = (long long)d.nx * d.ny * d.nz;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n;
+       e += (long long)gridDim.x * 256) {
+    const int x = (int)(e % d.nx);
+    const long long r = e / d.nx;
+    const int y = (int)(r % d.ny), z = (int)(r / d.ny);
+    global[e] = recv[chunk_pos(d, x, y, z)];
+  }
+}
+
+// tmp3d = sgemv('n', n2d*nz_ph, k, 1.0/(g*k), ph, ., x = 1, 0.0) in the reference BLAS
+// order (y = 0; y += (alpha*x(j)) * A(:,j) for j = 1..k), then (:500-505)
+//   stagger 1: alt = tmp3d;  stagger 0: alt = (tmp3d(:,:,2:nz_ph) + tmp3d(:,:,1:nz)) * 0.5
+__device__ inline float member_mean(const float *__restrict__ ph, long long stride, int k,
+                                    float alpha, long long at) {
+  float y = 0.0f;
+  for (int m = 0; m < k; ++m) y = y + alpha * ph[at + m * stride];
+  return y;
+}
+
+__global__ void __launch_bounds__(256)
+vcoord_mean_kernel(const float *__restrict__ ph, long long n2d, int nz_ph, int k, int stagger,
+                   float alpha, float *__restrict__ alt) {
+  const int nz_out = stagger == 1 ? nz_ph : nz_ph - 1;
+  const long long stride = n2d * nz_ph;  // member stride of ph(n2d, nz_ph, 0:k-1)
+  const long long n = n2d * nz_out;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n;
+       e += (long long)gridDim.x * 256) {
+    if (stagger == 1) {
+      alt[e] = member_mean(ph, stride, k, alpha, e);
+    } else {
+      const float lo = member_mean(ph, stride, k, alpha, e);
+      const float hi = member_mean(ph, stride, k, alpha, e + n2d);
+      alt[e] = (hi + lo) * 0.5f;
+    }
+  }
+}
+
+static dim3 grid_for(long long n) {
+  const long long b = (n + 255) / 256;
+  return dim3((unsigned)std::min<long long>(std::max<long long>(b, 1), 1 << 20));
+}
+
+hipError_t launch_pack_columns(hipStream_t s, const float *global, const Decomp &d,
+                               float *send) {
+  const long long n = (long long)d.nx * d.ny * d.nz;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_columns_kernel, grid_for(n), dim3(256), 0, s, global, d, send);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_columns(hipStream_t s, const float *recv, const Decomp &d,
+                                 float *global) {
+  const long long n = (long long)d.nx * d.ny * d.nz;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(unpack_columns_kernel, grid_for(n), dim3(256), 0, s, recv, d, global);
+  return hipGetLastError();
+}
+
+hipError_t launch_vcoord_mean(hipStream_t s, const float *ph, long long n2d, int nz_ph, int k,
+                              int stagger, float alpha, float *alt) {
+  const long long n = n2d * (stagger == 1 ? nz_ph : nz_ph - 1);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(vcoord_mean_kernel, grid_for(n), dim3(256), 0, s, ph, n2d, nz_ph, k,
+                     stagger, alpha, alt);
+  return hipGetLastError();
+}
+
+}  // namespace cwbl

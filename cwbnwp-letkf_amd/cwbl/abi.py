@@ -85,6 +85,7 @@ class Stats(C.Structure):
 
 #: exported symbols of the product library (include/cwb_letkf_core.h)
 EXPORTS = ["cwbl_init", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch", "cwbl_search",
+           "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
            "cwbl_finalize", "cwbl_last_error", "cwbl_abi_version"]
 
 
@@ -222,11 +223,15 @@ def load_library(path=None):
                                      C.c_int, C.c_float, vp, vp, C.c_int]
     lib.cwbl_search.argtypes = [C.c_int, vp, C.c_float, C.c_float, C.c_int, C.c_int, vp, vp,
                                 vp, vp, C.c_int]
+    lib.cwbl_pack_columns.argtypes = [vp] + [C.c_int] * 5 + [vp]
+    lib.cwbl_unpack_columns.argtypes = [vp] + [C.c_int] * 5 + [vp]
+    lib.cwbl_vcoord_mean.argtypes = [vp, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_float, vp]
     lib.cwbl_finalize.argtypes = []
     lib.cwbl_last_error.restype = cp
     lib.cwbl_abi_version.restype = C.c_int
     for fn in ("cwbl_init", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch",
-               "cwbl_search", "cwbl_finalize"):
+               "cwbl_search", "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
+               "cwbl_finalize"):
         getattr(lib, fn).restype = C.c_int
     return lib
 
@@ -284,6 +289,21 @@ class Core:
                                          max_lz_pts, nq, _ptr(q_xyz), _ptr(nf), _ptr(idx),
                                          _ptr(r2), MEM_HOST))
         return nf, idx, r2
+
+    # ---- member <-> column transposes (device pointers; see cwbl/transpose.py) ----------
+    def pack_columns(self, global_field, nx, ny, nz, px, py, send):
+        """letkf_scatter_grid's send-side packing (module_mpi_util.f90:224-258)."""
+        self._check(self.lib.cwbl_pack_columns(_ptr(global_field), nx, ny, nz, px, py,
+                                               _ptr(send)))
+
+    def unpack_columns(self, recv, nx, ny, nz, px, py, global_field):
+        """letkf_gather_grid's receive-side unpacking (module_mpi_util.f90:326-350)."""
+        self._check(self.lib.cwbl_unpack_columns(_ptr(recv), nx, ny, nz, px, py,
+                                                 _ptr(global_field)))
+
+    def vcoord_mean(self, ph, n2d, nz_ph, k, stagger, g, alt):
+        """letkf_scatter_vcoord's member mean of PH/g + destagger (:491-505)."""
+        self._check(self.lib.cwbl_vcoord_mean(_ptr(ph), n2d, nz_ph, k, stagger, g, _ptr(alt)))
 
     def finalize(self):
         self._check(self.lib.cwbl_finalize())

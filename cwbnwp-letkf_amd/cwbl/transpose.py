@@ -1,0 +1,249 @@
+"""Member <-> column transposes on the device.
+
+The reference moves every analysed variable between two layouts with host-packed MPI
+collectives (module_mpi_util.f90):
+  member layout  rank m holds member m's whole field, global(nx,ny,nz)
+  column layout  each rank holds its columns for all members, var(loc_nx,loc_ny,nz,0:k-1)
+  letkf_scatter_grid   (:190-262)  member -> column  (mpi_alltoallv)
+  letkf_gather_grid    (:264-358)  column -> member  (mpi_alltoallv)
+  letkf_scatter_hcoord (:360-443)  root's lat/lon -> columns (mpi_scatterv)
+  letkf_scatter_vcoord (:445-580)  member PH -> column ensemble mean / g, destaggered
+                                   (mpi_alltoallv + sgemv), or root's HGT (mpi_scatterv)
+Columns are dealt cyclically with block 1 over a px x py rank grid (letkf_local_info,
+:71-188, px >= py from mpi_dims_create).
+
+Here the packing, unpacking and the ensemble mean are HIP kernels behind the C ABI
+(cwbl_pack_columns / cwbl_unpack_columns / cwbl_vcoord_mean) working on device memory, and
+the exchange is torch.distributed point-to-point: with backend "nccl" (RCCL on ROCm) one
+group of ncclSend/ncclRecv over xGMI per transpose, messages going straight from the packed
+buffer into their final place in `var` (member-slowest, so each member's chunk is
+contiguous: no unpack on the column side).  Backend "gloo" stages each message through host
+memory; it is the transport of the CPU/one-GPU multi-process tests, not a compute path.
+
+Member m lives on rank m % world: the reference's rank m when world >= k, and k/world
+members per rank on an 8-GPU node at k = 40.
+Tensors: a global field is torch (nz, ny', nx') for Fortran global(nx',ny',nz); a column slab
+is (k, nz, loc_ny, loc_nx) for var(loc_nx,loc_ny,nz,0:k-1).
+"""
+import math
+
+import numpy as np
+
+G = 9.81  # module_param.f90:109
+
+
+def dims_create(nproc):
+    """MPI_Dims_create(nproc, 2): the most balanced (px, py), px >= py (letkf_init :48-52)."""
+    d = next(d for d in range(math.isqrt(nproc), nproc + 1) if d * d >= nproc and nproc % d == 0)
+    return d, nproc // d
+
+
+def _cyc(n, i, p):
+    return (n - i + p - 1) // p if i < n else 0
+
+
+class Decomposition:
+    """letkf_local_info (:71-188) for an nx x ny mass grid over `world` ranks."""
+
+    def __init__(self, nx, ny, world):
+        self.nx, self.ny, self.world = nx, ny, world
+        self.px, self.py = dims_create(world)
+
+    def grid(self, stagger):
+        """(nx', ny') of the field: U is staggered in x (stagger 1), V in y (stagger 2)."""
+        return self.nx + (stagger == 1), self.ny + (stagger == 2)
+
+    def coords(self, rank):
+        return rank % self.px, rank // self.px
+
+    def local_shape(self, rank, stagger=0):
+        """(loc_nx, loc_ny), or (loc_nx_u, loc_ny) / (loc_nx, loc_ny_v) when staggered."""
+        gx, gy = self.grid(stagger)
+        ix, iy = self.coords(rank)
+        return _cyc(gx, ix, self.px), _cyc(gy, iy, self.py)
+
+    def columns(self, rank, stagger=0):
+        """0-based xloc, yloc of `rank` (cpu(rank)%xloc - 1, ...)."""
+        gx, gy = self.grid(stagger)
+        ix, iy = self.coords(rank)
+        return np.arange(ix, gx, self.px), np.arange(iy, gy, self.py)
+
+    def chunks(self, nz, stagger=0):
+        """(offset, count) of every rank's chunk in a packed buffer (sdispls/sendcnts)."""
+        out, off = [], 0
+        for r in range(self.world):
+            lx, ly = self.local_shape(r, stagger)
+            out.append((off, lx * ly * nz))
+            off += lx * ly * nz
+        return out
+
+
+class Transposer:
+    """One rank's side of the transposes.  `core` is the cwbl.abi.Core of this process."""
+
+    def __init__(self, core, k, nx, ny, group=None, device=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.core, self.k, self.group = core, k, group
+        if dist.is_available() and dist.is_initialized():
+            self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+            self.backend = dist.get_backend(group)
+        else:
+            self.rank, self.world, self.backend = 0, 1, None
+        self.dec = Decomposition(nx, ny, self.world)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+
+    # ---- ownership -------------------------------------------------------------------------
+    def owner(self, m):
+        return m % self.world
+
+    def owned(self):
+        return list(range(self.rank, self.k, self.world))
+
+    def local_shape(self, stagger=0):
+        return self.dec.local_shape(self.rank, stagger)
+
+    # ---- transport -------------------------------------------------------------------------
+    def _peer(self, r):
+        return r if self.group is None else self.dist.get_global_rank(self.group, r)
+
+    def _exchange(self, sends, recvs):
+        """sends / recvs: lists of (peer rank, tag, contiguous device tensor); posted in the
+        same (peer, tag) order on both sides."""
+        dist, torch = self.dist, self.torch
+        if not sends and not recvs:
+            return
+        if self.backend == "nccl":
+            ops = [dist.P2POp(dist.isend, t, self._peer(p), self.group) for p, _, t in sends]
+            ops += [dist.P2POp(dist.irecv, t, self._peer(p), self.group) for p, _, t in recvs]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            return
+        # gloo (tests): host staging, one tag per message
+        reqs, landing = [], []
+        for p, tag, t in sends:
+            h = t.cpu()
+            reqs.append((dist.isend(h, self._peer(p), group=self.group, tag=tag), h))
+        for p, tag, t in recvs:
+            h = torch.empty(t.shape, dtype=t.dtype)
+            reqs.append((dist.irecv(h, self._peer(p), group=self.group, tag=tag), h))
+            landing.append((h, t))
+        for w, _ in reqs:
+            w.wait()
+        for h, t in landing:
+            t.copy_(h)
+
+    def _sync(self):
+        # the library runs on its own stream: torch's producers must have finished
+        if self.device.type == "cuda":
+            self.torch.cuda.synchronize(self.device)
+
+    # ---- letkf_scatter_grid (:190-262) ---------------------------------------------------------
+    def scatter_grid(self, fields, nz, stagger=0, out=None):
+        """fields: {m: (nz, ny', nx') device tensor} for the members this rank owns.
+        Returns var (k, nz, loc_ny, loc_nx) with every member's columns of this rank."""
+        torch = self.torch
+        gx, gy = self.dec.grid(stagger)
+        lx, ly = self.local_shape(stagger)
+        var = out if out is not None else torch.empty((self.k, nz, ly, lx), dtype=torch.float32,
+                                                       device=self.device)
+        chunks = self.dec.chunks(nz, stagger)
+        self._sync()
+        sends, recvs, keep = [], [], []
+        for m in range(self.k):
+            src = self.owner(m)
+            if src == self.rank:
+                f = fields[m]
+                assert f.is_contiguous() and tuple(f.shape) == (nz, gy, gx), (m, tuple(f.shape))
+                packed = torch.empty(gx * gy * nz, dtype=torch.float32, device=self.device)
+                self.core.pack_columns(f, gx, gy, nz, self.dec.px, self.dec.py, packed)
+                keep.append(packed)
+                for d, (off, cnt) in enumerate(chunks):
+                    if d == self.rank:
+                        var[m].view(-1).copy_(packed[off:off + cnt])
+                    elif cnt:
+                        sends.append((d, m, packed[off:off + cnt]))
+            elif lx * ly * nz:
+                recvs.append((src, m, var[m].view(-1)))
+        self._exchange(sends, recvs)
+        self._sync()
+        return var
+
+    # ---- letkf_gather_grid (:264-358) ------------------------------------------------------------
+    def gather_grid(self, var, stagger=0, out=None):
+        """var (k, nz, loc_ny, loc_nx) -> {m: (nz, ny', nx')} for the members this rank owns."""
+        torch = self.torch
+        k, nz = var.shape[:2]
+        gx, gy = self.dec.grid(stagger)
+        chunks = self.dec.chunks(nz, stagger)
+        out = out if out is not None else {}
+        self._sync()
+        sends, recvs, packed = [], [], {}
+        for m in range(k):
+            dst = self.owner(m)
+            if dst == self.rank:
+                buf = torch.empty(gx * gy * nz, dtype=torch.float32, device=self.device)
+                packed[m] = buf
+                for s, (off, cnt) in enumerate(chunks):
+                    if s == self.rank:
+                        buf[off:off + cnt].copy_(var[m].reshape(-1))
+                    elif cnt:
+                        recvs.append((s, m, buf[off:off + cnt]))
+            elif var[m].numel():
+                sends.append((dst, m, var[m].reshape(-1).contiguous()))
+        self._exchange(sends, recvs)
+        self._sync()
+        for m, buf in packed.items():
+            g = out.get(m)
+            if g is None:
+                g = out[m] = torch.empty((nz, gy, gx), dtype=torch.float32, device=self.device)
+            self.core.unpack_columns(buf, gx, gy, nz, self.dec.px, self.dec.py, g)
+        return out
+
+    # ---- root -> columns (letkf_scatter_hcoord :360-443, vcoord stagger -1 :543-575) ----------
+    def scatter_from_root(self, field, nz=1, stagger=0, root=0):
+        """field (nz, ny', nx') on `root` (ignored elsewhere) -> (nz, loc_ny, loc_nx)."""
+        torch = self.torch
+        gx, gy = self.dec.grid(stagger)
+        lx, ly = self.local_shape(stagger)
+        local = torch.empty((nz, ly, lx), dtype=torch.float32, device=self.device)
+        chunks = self.dec.chunks(nz, stagger)
+        self._sync()
+        sends, recvs, keep = [], [], []
+        if self.rank == root:
+            assert field.is_contiguous() and tuple(field.shape) == (nz, gy, gx)
+            packed = torch.empty(gx * gy * nz, dtype=torch.float32, device=self.device)
+            self.core.pack_columns(field, gx, gy, nz, self.dec.px, self.dec.py, packed)
+            keep.append(packed)
+            for d, (off, cnt) in enumerate(chunks):
+                if d == root:
+                    local.view(-1).copy_(packed[off:off + cnt])
+                elif cnt:
+                    sends.append((d, 0, packed[off:off + cnt]))
+        elif local.numel():
+            recvs.append((root, 0, local.view(-1)))
+        self._exchange(sends, recvs)
+        self._sync()
+        return local
+
+    def scatter_hcoord(self, lat, lon, stagger=0, root=0):
+        """letkf_scatter_hcoord: root's (ny', nx') lat/lon -> this rank's columns."""
+        one = lambda f: None if f is None else f.reshape((1,) + tuple(f.shape[-2:]))  # noqa: E731
+        return (self.scatter_from_root(one(lat), 1, stagger, root)[0],
+                self.scatter_from_root(one(lon), 1, stagger, root)[0])
+
+    # ---- letkf_scatter_vcoord (:445-580) ---------------------------------------------------------
+    def scatter_vcoord(self, fields, nz, stagger, g=G, root=0):
+        """alt (nz, loc_ny, loc_nx) on the mass-grid columns.
+        stagger 0/1: fields = {m: PH (nz_ph, ny, nx)} of the owned members, nz_ph = nz + 1
+        (0: destaggered to mass levels) or nz (1: W/PH levels); the ensemble mean over all
+        k members divided by g.  stagger -1: fields = HGT (1, ny, nx) on `root`."""
+        if stagger == -1:
+            return self.scatter_from_root(fields, 1, 0, root)
+        nz_ph = nz if stagger == 1 else nz + 1
+        tmp4d = self.scatter_grid(fields, nz_ph, 0)
+        lx, ly = self.local_shape(0)
+        alt = self.torch.empty((nz, ly, lx), dtype=self.torch.float32, device=self.device)
+        self.core.vcoord_mean(tmp4d, lx * ly, nz_ph, self.k, 1 if stagger == 1 else 0, g, alt)
+        return alt

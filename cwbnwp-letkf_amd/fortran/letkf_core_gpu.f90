@@ -69,6 +69,7 @@ module letkf_core_gpu
     end type cwbl_stats
 
     public :: cwbl_init, cwbl_set_obs, cwbl_analyze_var, cwbl_solve_batch, cwbl_search, &
+              cwbl_pack_columns, cwbl_unpack_columns, cwbl_vcoord_mean, &
               cwbl_finalize, cwbl_abi_version, cwbl_error, cwbl_check
 
     interface
@@ -104,6 +105,30 @@ module letkf_core_gpu
             real(c_float),  value :: hclr, vclr
             type(c_ptr),    value :: obs_xyz, q_xyz, nfound, idx, r2
         end function cwbl_search
+
+        ! member <-> column transposes (module_mpi_util.f90:190-358, 445-580); device pointers
+        integer(c_int) function cwbl_pack_columns(global, nx, ny, nz, px, py, send) &
+                bind(C, name='cwbl_pack_columns')
+            import :: c_int, c_ptr
+            type(c_ptr),    value :: global, send
+            integer(c_int), value :: nx, ny, nz, px, py
+        end function cwbl_pack_columns
+
+        integer(c_int) function cwbl_unpack_columns(recv, nx, ny, nz, px, py, global) &
+                bind(C, name='cwbl_unpack_columns')
+            import :: c_int, c_ptr
+            type(c_ptr),    value :: recv, global
+            integer(c_int), value :: nx, ny, nz, px, py
+        end function cwbl_unpack_columns
+
+        integer(c_int) function cwbl_vcoord_mean(ph, n2d, nz_ph, k, stagger, g, alt) &
+                bind(C, name='cwbl_vcoord_mean')
+            import :: c_int, c_long_long, c_float, c_ptr
+            type(c_ptr),          value :: ph, alt
+            integer(c_long_long), value :: n2d
+            integer(c_int),       value :: nz_ph, k, stagger
+            real(c_float),        value :: g
+        end function cwbl_vcoord_mean
 
         integer(c_int) function cwbl_finalize() bind(C, name='cwbl_finalize')
             import :: c_int

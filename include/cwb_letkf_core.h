@@ -203,6 +203,32 @@ int         cwbl_search(int nobs, const float *obs_xyz, float hclr, float vclr,
                         int max_lz_pts, int nq, const float *q_xyz,
                         int *nfound, int *idx, float *r2, int memory);
 
+/* ---- member <-> column transposes -----------------------------
+ * The reference moves each variable between member layout (rank m holds member m's field
+ * global(nx,ny,nz)) and column layout (each rank holds var(loc_nx,loc_ny,nz,0:k-1) for its
+ * columns) with mpi_alltoallv (module_mpi_util.f90:190-358).  Columns are split cyclically,
+ * block 1, over a px x py rank grid (letkf_local_info, :71-188; px >= py from
+ * mpi_dims_create): rank r = id_x + id_y*px owns x = id_x + i*px, y = id_y + j*py (0-based).
+ * The exchange itself is RCCL point-to-point (cwbl/transpose.py); these entry points do the
+ * packing in device memory (all pointers are device pointers; px, py <= 64; each call has
+ * completed when it returns). */
+
+/* letkf_scatter_grid's send side (:224-258): global(nx,ny,nz) -> send, the rank-major
+ * concatenation of global(xloc_r, yloc_r, :) for r = 0..px*py-1, each chunk
+ * (loc_nx_r, loc_ny_r, nz) in Fortran order. */
+int         cwbl_pack_columns(const float *global, int nx, int ny, int nz, int px, int py,
+                              float *send);
+/* letkf_gather_grid's receive side (:326-350): the inverse of cwbl_pack_columns. */
+int         cwbl_unpack_columns(const float *recv, int nx, int ny, int nz, int px, int py,
+                                float *global);
+/* letkf_scatter_vcoord's reduction (:491-505): ph(n2d, nz_ph, 0:k-1), member slowest ->
+ * alt(n2d, nz_out).  tmp = sgemv('n', n2d*nz_ph, k, 1.0/(g*k), ph, ., ones, 0.0) evaluated
+ * in the reference BLAS order (y = 0; y += (alpha*1)*ph(:,m), m = 0..k-1, fp32); then
+ * stagger 1: alt = tmp (nz_out = nz_ph); stagger 0: alt = (tmp(:,2:) + tmp(:,:nz_ph-1))*0.5
+ * (nz_out = nz_ph - 1). */
+int         cwbl_vcoord_mean(const float *ph, long long n2d, int nz_ph, int k, int stagger,
+                             float g, float *alt);
+
 int         cwbl_finalize(void);
 const char *cwbl_last_error(void);
 int         cwbl_abi_version(void);

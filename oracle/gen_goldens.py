@@ -13,8 +13,10 @@ Fixtures
   G3 gc.npz                Gaspari_Cohn_1999 (module_localization.f90:333-364)
   G4 driver_*.npz          one variable through the driver loop (module_letkf_core.f90:59-240)
   G5 tune_q.npz            letkf_tune_q KATs (module_letkf_core.f90:702-733), incl. Q3 columns
+  G6 dims_create.json      MPI_Dims_create(n, 2) from the MPICH the reference links
+                           (/opt/conda/lib/libmpi.so), as letkf_init calls it (module_mpi_util.f90:48-49)
 
-`python oracle/gen_goldens.py tuneq` regenerates only G5 (and updates its manifest entry).
+`python oracle/gen_goldens.py tuneq` / `dims` regenerate only G5 / G6 (and their manifest entries).
 """
 import json
 import os
@@ -263,6 +265,28 @@ def main_tuneq():
     print(json.dumps(manifest["files"]["tune_q.npz"], indent=1))
 
 
+def main_dims():
+    """G6: MPICH's MPI_Dims_create(n, 2) for n = 1..128 (a singleton MPI_Init, no mpirun)."""
+    import ctypes as C
+    lib = C.CDLL(os.environ.get("MPI_LIB", "/opt/conda/lib/libmpi.so"), mode=C.RTLD_GLOBAL)
+    assert lib.MPI_Init(None, None) == 0
+    out = {}
+    for n in range(1, 129):
+        d = (C.c_int * 2)(0, 0)
+        assert lib.MPI_Dims_create(n, 2, d) == 0
+        out[str(n)] = [d[0], d[1]]
+    lib.MPI_Finalize()
+    with open(os.path.join(OUT, "dims_create.json"), "w") as f:
+        json.dump({"source": "MPICH MPI_Dims_create(n, 2, dims) with dims = 0, "
+                   "/opt/conda/lib/libmpi.so", "dims": out}, f, sort_keys=True)
+    mpath = os.path.join(OUT, "MANIFEST.json")
+    with open(mpath) as f:
+        manifest = json.load(f)
+    manifest["files"]["dims_create.json"] = {"what": "G6 MPI_Dims_create(n, 2), n = 1..128"}
+    with open(mpath, "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build oracle/_ref/ref_harness first (make -C oracle ref)")
@@ -354,6 +378,9 @@ def main():
 if __name__ == "__main__":
     if sys.argv[1:] == ["tuneq"]:
         main_tuneq()
+    elif sys.argv[1:] == ["dims"]:
+        main_dims()
     else:
         main()
         main_tuneq()
+        main_dims()

@@ -1,0 +1,106 @@
+"""GPU checks of the member <-> column transposes: the HIP packing
+kernels and the ensemble-mean kernel against the oracle (oracle/mpi_util_oracle.py), and
+the whole Transposer with the real kernels over 2 processes on one GPU (gloo transport)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cwbl import abi
+from cwbl import transpose as tr
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+import mpi_util_oracle as mo  # noqa: E402
+from test_transpose import check_plan, run_plan  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+_core = {}
+
+
+def core(k=8):
+    if _core.get("k") != k:
+        if "c" in _core:
+            _core["c"].finalize()
+        _core["c"] = abi.Core(k, device=0)
+        _core["k"] = k
+    return _core["c"]
+
+
+@pytest.mark.parametrize("nz,ny,nx,world", [(3, 7, 10, 1), (3, 7, 10, 6), (5, 11, 9, 8),
+                                            (2, 3, 5, 8), (4, 33, 65, 12), (50, 300, 301, 8)])
+def test_pack_unpack_vs_oracle(nz, ny, nx, world):
+    c = core()
+    px, py = tr.dims_create(world)
+    f = torch.randn((nz, ny, nx), device="cuda", dtype=torch.float32)
+    send = torch.full((nz * ny * nx,), float("nan"), device="cuda")
+    c.pack_columns(f, nx, ny, nz, px, py, send)
+    want = mo.pack_columns(f.cpu().numpy(), px, py)
+    np.testing.assert_array_equal(send.cpu().numpy(), want)
+    back = torch.full_like(f, float("nan"))
+    c.unpack_columns(send, nx, ny, nz, px, py, back)
+    assert torch.equal(back, f)
+
+
+@pytest.mark.parametrize("k,stagger", [(8, 0), (40, 0), (40, 1), (128, 0)])
+def test_vcoord_mean_vs_oracle(k, stagger):
+    c = core()
+    rng = np.random.default_rng(k + stagger)
+    nz_ph, ly, lx = 11, 9, 13
+    # geopotential-like magnitudes: level * 3000 m^2/s^2 plus member spread
+    ph = (np.arange(nz_ph, dtype=np.float32)[None, :, None, None] * 3000.0 +
+          rng.normal(0, 50, (k, nz_ph, ly, lx))).astype(np.float32)
+    nz_out = nz_ph if stagger == 1 else nz_ph - 1
+    alt = torch.empty((nz_out, ly, lx), device="cuda")
+    c.vcoord_mean(torch.from_numpy(ph).cuda(), lx * ly, nz_ph, k, stagger, tr.G, alt)
+    got = alt.cpu().numpy()
+    np.testing.assert_array_equal(got, mo.vcoord_mean(ph, stagger))   # reference BLAS order
+    mkl = mo.mkl_sgemv_mean(ph, stagger)
+    if mkl is not None:   # the reference's own sgemv call (MKL_CBWR=COMPATIBLE)
+        np.testing.assert_array_equal(got, mkl)
+
+
+def test_transposer_local_world1():
+    """world 1: every transfer is a self copy; the packing kernels do all the work."""
+    c = core(5)
+    t = tr.Transposer(c, 5, 7, 6)
+    nz = 4
+    members = [torch.randn((nz, 6, 7), device="cuda") for _ in range(5)]
+    var = t.scatter_grid({m: members[m] for m in range(5)}, nz)
+    assert torch.equal(var, torch.stack(members))   # one rank owns every column
+    back = t.gather_grid(var)
+    for m in range(5):
+        assert torch.equal(back[m], members[m])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out_dir, k, nx, ny, nz):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    c = abi.Core(k, device=0)
+    t = tr.Transposer(c, k, nx, ny)
+    run_plan(t, k, nx, ny, nz, out_dir, rank)
+    dist.barrier()
+    c.finalize()
+    dist.destroy_process_group()
+
+
+def test_transposer_two_processes_real_kernels(tmp_path):
+    world, k, nx, ny, nz = 2, 5, 7, 5, 3
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), k, nx, ny, nz), nprocs=world,
+             join=True)
+    check_plan(str(tmp_path), world, k, nx, ny, nz)

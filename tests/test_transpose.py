@@ -1,0 +1,173 @@
+"""CPU checks of the member <-> column transposes (cwbl/transpose.py):
+the decomposition against MPICH's MPI_Dims_create (G6) and the reference's letkf_local_info
+loops (oracle/mpi_util_oracle.py), and the exchange plan over gloo with world sizes 2 and 3.
+
+On CPU the HIP packing kernels are unavailable, so the gloo tests hand the Transposer a
+stand-in `core` whose pack/unpack/mean are the oracle's (test-only injection; the product
+Transposer takes the real cwbl.abi.Core, whose init fails without a GPU).  The same plan with
+the real kernels runs in tests/test_gpu_transpose.py."""
+import json
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cwbl import transpose as tr
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import mpi_util_oracle as mo  # noqa: E402
+
+
+def test_dims_create_matches_mpich():
+    with open(os.path.join(HERE, "golden", "dims_create.json")) as f:
+        g = json.load(f)["dims"]
+    for n, d in g.items():
+        assert list(tr.dims_create(int(n))) == d, n
+        assert list(mo.dims_create(int(n))) == d, n
+
+
+@pytest.mark.parametrize("nx,ny,world", [(10, 7, 1), (10, 7, 2), (9, 11, 4), (5, 3, 8),
+                                         (300, 300, 8), (2, 2, 6)])
+def test_decomposition_matches_local_info(nx, ny, world):
+    dec = tr.Decomposition(nx, ny, world)
+    for r, info in enumerate(mo.local_info(nx, ny, world)):
+        for st, (xk, yk) in ((0, ("xloc", "yloc")), (1, ("xloc_u", "yloc")),
+                             (2, ("xloc", "yloc_v"))):
+            xl, yl = dec.columns(r, st)
+            np.testing.assert_array_equal(xl, info[xk])
+            np.testing.assert_array_equal(yl, info[yk])
+            assert dec.local_shape(r, st) == (len(info[xk]), len(info[yk]))
+    # every column exactly once
+    for st in (0, 1, 2):
+        gx, gy = dec.grid(st)
+        assert sum(a * b for a, b in (dec.local_shape(r, st) for r in range(world))) == gx * gy
+        offs = dec.chunks(3, st)
+        assert offs[-1][0] + offs[-1][1] == gx * gy * 3
+
+
+def test_oracle_pack_is_scatter_order():
+    rng = np.random.default_rng(3)
+    nz, ny, nx, world = 3, 7, 10, 6
+    f = rng.normal(size=(nz, ny, nx)).astype(np.float32)
+    px, py = mo.dims_create(world)
+    packed = mo.pack_columns(f, px, py)
+    per_rank = mo.scatter_grid([f], world)
+    np.testing.assert_array_equal(packed, np.concatenate([v[0].ravel() for v in per_rank]))
+    np.testing.assert_array_equal(mo.unpack_columns(packed, nz, ny, nx, px, py), f)
+
+
+class OracleCore:
+    """Test stand-in for cwbl.abi.Core's transpose entry points (CPU tensors)."""
+
+    def pack_columns(self, g, nx, ny, nz, px, py, send):
+        send.copy_(torch.from_numpy(mo.pack_columns(g.numpy().reshape(nz, ny, nx), px, py)))
+
+    def unpack_columns(self, recv, nx, ny, nz, px, py, g):
+        g.copy_(torch.from_numpy(mo.unpack_columns(recv.numpy(), nz, ny, nx, px, py)))
+
+    def vcoord_mean(self, ph, n2d, nz_ph, k, stagger, gconst, alt):
+        alt.copy_(torch.from_numpy(mo.vcoord_mean(ph.numpy(), stagger, np.float32(gconst))))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def fields_for(k, nz, gy, gx, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.normal(size=(nz, gy, gx)).astype(np.float32) for _ in range(k)]
+
+
+def run_plan(t, k, nx, ny, nz, out_dir, rank):
+    """Scatter (mass, U, V grids), gather, vcoord (0, 1, -1) and hcoord; save per rank."""
+    res = {}
+    for st in (0, 1, 2):
+        gx, gy = t.dec.grid(st)
+        members = fields_for(k, nz, gy, gx, 10 + st)
+        own = {m: torch.from_numpy(members[m]).to(t.device) for m in t.owned()}
+        var = t.scatter_grid(own, nz, st)
+        res[f"var{st}"] = var.cpu().numpy()
+        back = t.gather_grid(var * 2.0, st)
+        for m in t.owned():
+            res[f"back{st}_{m}"] = back[m].cpu().numpy()
+    ph = fields_for(k, nz + 1, ny, nx, 30)
+    own = {m: torch.from_numpy(ph[m]).to(t.device) for m in t.owned()}
+    res["alt0"] = t.scatter_vcoord(own, nz, 0).cpu().numpy()
+    own1 = {m: torch.from_numpy(ph[m][:nz].copy()).to(t.device) for m in t.owned()}
+    res["alt1"] = t.scatter_vcoord(own1, nz, 1).cpu().numpy()
+    hgt = torch.from_numpy(ph[0][:1].copy()).to(t.device) if rank == 0 else None
+    res["altm1"] = t.scatter_vcoord(hgt, 1, -1).cpu().numpy()
+    ll = fields_for(2, 1, ny, nx + 1, 40)   # U-grid lat/lon (stagger 1)
+    lat = torch.from_numpy(ll[0][0].copy()).to(t.device) if rank == 0 else None
+    lon = torch.from_numpy(ll[1][0].copy()).to(t.device) if rank == 0 else None
+    la, lo = t.scatter_hcoord(lat, lon, 1)
+    res["lat"], res["lon"] = la.cpu().numpy(), lo.cpu().numpy()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
+
+
+def check_plan(out_dir, world, k, nx, ny, nz):
+    res = [dict(np.load(os.path.join(out_dir, f"rank{r}.npz"))) for r in range(world)]
+    for st in (0, 1, 2):
+        gx, gy = nx + (st == 1), ny + (st == 2)
+        members = fields_for(k, nz, gy, gx, 10 + st)
+        want = mo.scatter_grid(members, world, st)
+        for r in range(world):
+            np.testing.assert_array_equal(res[r][f"var{st}"], want[r])
+            for m in range(r, k, world):
+                np.testing.assert_array_equal(res[r][f"back{st}_{m}"], members[m] * 2.0)
+    ph = fields_for(k, nz + 1, ny, nx, 30)
+    tmp0 = mo.scatter_grid(ph, world, 0)
+    tmp1 = mo.scatter_grid([p[:nz] for p in ph], world, 0)
+    hg = mo.scatter_grid([ph[0][:1]], world, 0)
+    ll = fields_for(2, 1, ny, nx + 1, 40)
+    lat = mo.scatter_grid([ll[0]], world, 1)
+    lon = mo.scatter_grid([ll[1]], world, 1)
+    for r in range(world):
+        np.testing.assert_array_equal(res[r]["alt0"], mo.vcoord_mean(tmp0[r], 0))
+        np.testing.assert_array_equal(res[r]["alt1"], mo.vcoord_mean(tmp1[r], 1))
+        np.testing.assert_array_equal(res[r]["altm1"], hg[r][0])
+        np.testing.assert_array_equal(res[r]["lat"], lat[r][0, 0])
+        np.testing.assert_array_equal(res[r]["lon"], lon[r][0, 0])
+
+
+def _worker(rank, world, port, out_dir, k, nx, ny, nz):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = tr.Transposer(OracleCore(), k, nx, ny, device=torch.device("cpu"))
+    run_plan(t, k, nx, ny, nz, out_dir, rank)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k", [(2, 5), (3, 4)])
+def test_transposes_gloo(tmp_path, world, k):
+    nx, ny, nz = 7, 5, 3
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), k, nx, ny, nz), nprocs=world,
+             join=True)
+    check_plan(str(tmp_path), world, k, nx, ny, nz)
+
+
+@pytest.mark.parametrize("k,stagger", [(3, 0), (17, 1), (40, 0), (64, 1)])
+def test_oracle_vcoord_mean_matches_mkl_sgemv(k, stagger):
+    """Pins the oracle's mean: the reference's sgemv call itself, through MKL in its
+    conditional-numerical-reproducibility COMPATIBLE mode, gives the same bits as the
+    reference-BLAS order the oracle (and the HIP kernel) evaluates."""
+    rng = np.random.default_rng(k)
+    shape = (k, 9, 12, 11)
+    ph = (np.arange(9, dtype=np.float32)[None, :, None, None] * 3000.0 +
+          rng.normal(0, 50, shape)).astype(np.float32)
+    mkl = mo.mkl_sgemv_mean(ph, stagger)
+    if mkl is None:
+        pytest.skip("MKL not available")
+    np.testing.assert_array_equal(mo.vcoord_mean(ph, stagger), mkl)
