@@ -69,6 +69,38 @@ def cpu_baseline(w, target_s=12.0):
                       f"LAPACK={lib.orc_lapack_name().decode()}"}
 
 
+def time_transposes(core, w, k, rank, world, dev):
+    """One letkf_scatter_grid + letkf_gather_grid of the whole variable (k members of
+    nx x ny x nz fp32) through cwbl/transpose.py: HIP packing + RCCL point-to-point.
+    Members are dealt m % world; max over ranks of one timed pass after one warm-up."""
+    from cwbl import transpose as tr
+    nx, ny, nz = w.extra["cfg"]["nx"], w.extra["cfg"]["ny"], w.nz
+    t = tr.Transposer(core, k, nx, ny, device=dev)
+    fields = {m: torch.randn((nz, ny, nx), device=dev) for m in t.owned()}
+    res = {}
+    for it in range(2):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        var = t.scatter_grid(fields, nz)
+        t1 = time.perf_counter()
+        back = t.gather_grid(var)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        res = {"scatter_ms": (t1 - t0) * 1e3, "gather_ms": (t2 - t1) * 1e3}
+    for m in t.owned():
+        assert torch.equal(back[m], fields[m]), "transpose round trip"
+    if world > 1:
+        v = torch.tensor([res["scatter_ms"], res["gather_ms"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        res = {"scatter_ms": float(v[0]), "gather_ms": float(v[1])}
+    gb = k * nx * ny * nz * 4 / 1e9
+    res.update(variable_gb=gb, px_py=list(tr.dims_create(world)),
+               scatter_gbs=gb / (res["scatter_ms"] * 1e-3), gather_gbs=gb / (res["gather_ms"] * 1e-3))
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,6 +108,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--transposes", action="store_true",
+                    help="also time one member<->column transpose of the variable (detail only)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -134,6 +168,8 @@ def main():
         elapsed, pts_total = float(t.item()), float(p.item())
     else:
         pts_total = float(pts_local)
+
+    tr_detail = time_transposes(core, w, k, rank, world, dev) if args.transposes else None
 
     if rank == 0:
         jacobi = os.environ.get("CWBL_SOLVER") == "jacobi"
@@ -198,6 +234,7 @@ def main():
                     sum(s.sweeps_sum for s in stats) / max(solved, 1),
                 "nonconverged": sum(s.nonconverged for s in stats),
                 "obs_bcast_ms": bcast_ms,
+                "transposes": tr_detail,
             },
             "cpu_baseline": None,
         }
