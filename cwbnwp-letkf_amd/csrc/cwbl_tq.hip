@@ -51,18 +51,33 @@ struct TqSmem {
   static constexpr int NB = KP / 4;
   static constexpr int PLD = 4 * NB + 4;  // pb row pitch: 2*PLD = 8*odd dwords, so the 8 block
                                           // rows of a half wave hit disjoint bank octets
+  // Trailing phase: from step J0T on, the remaining kTail x kTail matrix is held as 2x2
+  // blocks (NB2*(NB2+1)/2 = 55 <= 64 lanes), 4x fewer FMAs per lane than 4x4 blocks.
+  static constexpr int kTail = 20;
+  // (KP = 40 only: with more than one 4x4 block per lane the two phases' live ranges spill)
+  static constexpr int J0T = KP == 40 ? KP - kTail : KP;  // first step of the 2x2 phase
+  static constexpr int NB2 = kTail / 2;
+  static constexpr int NBLK2 = NB2 * (NB2 + 1) / 2;
+  static constexpr int PLD2 = 2 * NB2 + 2;  // 2x2-phase partials pitch (>= the packed tail)
+  static_assert(NB2 * PLD2 >= kTail * (kTail + 1) / 2 && NBLK2 <= 64, "tail layout");
   static constexpr int NHV = KP * (KP - 1) / 2;  // packed Householder vectors at k = KP
   static constexpr int hv_off(int j) { return j * (KP - 1) - j * (j - 1) / 2; }
-  static constexpr int cap() {  // region size: vectors so far + partials of rows >= j/4
+  static constexpr int cap() {  // region size: vectors so far + partials of the live rows
     int m = NHV + KP;
     for (int j = 0; j + 2 < KP; ++j) {
-      const int need = hv_off(j + 1) + (NB - j / 4) * PLD;
+      const int need = hv_off(j + 1) + (j < J0T ? (NB - j / 4) * PLD
+                                                : (NB2 - (j - J0T) / 2) * PLD2);
+      m = need > m ? need : m;
+    }
+    if (J0T < KP) {  // the packed tail at the switch (in the 2x2 partials' place)
+      const int need = hv_off(J0T) + NB2 * PLD2;
       m = need > m ? need : m;
     }
     return m;
   }
   static constexpr int REG = cap();
   static constexpr int pb_base(int J) { return REG - (NB - J) * PLD; }
+  static constexpr int pb2_base(int J2) { return REG - (NB2 - J2) * PLD2; }
   union {
     ColumnChunk<KP, kTqChunk, TqStage> ch;
     double ah[KP / 2][KP + 2];            // half of A on its way from MFMA tiles to blocks
@@ -224,31 +239,80 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   double ub = (lane < KP) ? b1acc : 0.0;                          // Yb d, becomes Q^T b1
 
   // ---- Householder tridiagonalisation (lower, dsytd2 order) ------------------------------
-  // Lane L keeps its lower 4x4 blocks (bi, bj) of A.  Per step j: the blocks of block
-  // column j/4 publish column j; lane i < KP forms v_i; every block adds its row and
-  // (transposed) column partial of A v into pb; lane i sums row i of pb; A -= v w^T + w v^T
-  // block by block.
+  // Lane L keeps its lower 4x4 blocks (bi, bj) of A; from step J0T on (KP >= 40) the
+  // trailing kTail x kTail matrix is re-dealt as 2x2 blocks (bi2, bj2), one per lane.  Per
+  // step j: the blocks of the pivot's block column publish column j; lane i < KP forms v_i;
+  // every block adds its row and (transposed) column partial of A v into pb; lane i sums row
+  // i of pb; A -= v w^T + w v^T block by block.
+  constexpr int J0T = SM::J0T, NB2 = SM::NB2, PLD2 = SM::PLD2;
+  int bi2 = 0, bj2 = 0;  // this lane's block of the 2x2 phase (lane < NBLK2)
+  while ((bi2 + 1) * (bi2 + 2) / 2 <= lane) ++bi2;
+  bj2 = lane - bi2 * (bi2 + 1) / 2;
+  const bool tail_lane = lane < SM::NBLK2;
   double trace = 0.0;
   auto ld4 = [](const double *p, double (&o)[4]) {
     const double2 a0 = *reinterpret_cast<const double2 *>(p);
     const double2 a1 = *reinterpret_cast<const double2 *>(p + 2);
     o[0] = a0.x; o[1] = a0.y; o[2] = a1.x; o[3] = a1.y;
   };
-  for (int j = 0; j < k; ++j) {
+  // One step of either phase.  The phases run as separate loops so that each keeps its own
+  // register assignment (one loop with a run-time phase test copies the blocks between
+  // registers every step).  The blocks are reached through the capture at NBL = 1 and
+  // through the parameter otherwise: the other way round, the compiler keeps them in scratch.
+  auto step = [&](const int j, auto phase, double (&Ap)[NBL][16]) __attribute__((always_inline)) {
+    constexpr bool ph2 = decltype(phase)::value;
+    double (&A)[NBL][16] = *[&]() {
+      if constexpr (NBL == 1) return &acc; else return &Ap;
+    }();
     const int J = j >> 2, qj = j & 3;
+    const int J2 = (j - J0T) >> 1, q2 = (j - J0T) & 1;
+    if constexpr (ph2) {
+      if (j == J0T) {  // re-deal the tail: 4x4 blocks -> packed lower triangle -> 2x2 blocks
+        double *tri = &sm.u.reg[J0T < KP ? SM::pb2_base(0) : 0];
+        constexpr int JB = J0T / 4;
 #pragma unroll
-    for (int it = 0; it < NBL; ++it) {
-      if (lane + 64 * it < NBLK && bj[it] == J) {  // publish column j
-        double cv[4];
-        switch (qj) {
-          case 0: for (int r = 0; r < 4; ++r) cv[r] = acc[it][4 * r]; break;
-          case 1: for (int r = 0; r < 4; ++r) cv[r] = acc[it][4 * r + 1]; break;
-          case 2: for (int r = 0; r < 4; ++r) cv[r] = acc[it][4 * r + 2]; break;
-          default: for (int r = 0; r < 4; ++r) cv[r] = acc[it][4 * r + 3]; break;
+        for (int it = 0; it < NBL; ++it) {
+          if (lane + 64 * it < NBLK && bi[it] >= JB && bj[it] >= JB) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const int a = 4 * (bi[it] - JB) + r, b = 4 * (bj[it] - JB) + q;
+                if (a >= b) tri[a * (a + 1) / 2 + b] = A[it][4 * r + q];
+              }
+          }
         }
-        *reinterpret_cast<double2 *>(&sm.col[4 * bi[it]]) = make_double2(cv[0], cv[1]);
-        *reinterpret_cast<double2 *>(&sm.col[4 * bi[it] + 2]) = make_double2(cv[2], cv[3]);
+        __syncthreads();
+        if (tail_lane) {
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int a = 2 * bi2 + r, b = 2 * bj2 + q;
+              A[0][2 * r + q] = a >= b ? tri[a * (a + 1) / 2 + b] : tri[b * (b + 1) / 2 + a];
+            }
+        }
+        __syncthreads();
       }
+    }
+    if constexpr (!ph2) {
+#pragma unroll
+      for (int it = 0; it < NBL; ++it) {
+        if (lane + 64 * it < NBLK && bj[it] == J) {  // publish column j
+          double cv[4];
+          switch (qj) {
+            case 0: for (int r = 0; r < 4; ++r) cv[r] = A[it][4 * r]; break;
+            case 1: for (int r = 0; r < 4; ++r) cv[r] = A[it][4 * r + 1]; break;
+            case 2: for (int r = 0; r < 4; ++r) cv[r] = A[it][4 * r + 2]; break;
+            default: for (int r = 0; r < 4; ++r) cv[r] = A[it][4 * r + 3]; break;
+          }
+          *reinterpret_cast<double2 *>(&sm.col[4 * bi[it]]) = make_double2(cv[0], cv[1]);
+          *reinterpret_cast<double2 *>(&sm.col[4 * bi[it] + 2]) = make_double2(cv[2], cv[3]);
+        }
+      }
+    } else if (tail_lane && bj2 == J2) {  // publish column j (2x2 phase)
+      const double c0 = q2 ? A[0][1] : A[0][0], c1 = q2 ? A[0][3] : A[0][2];
+      *reinterpret_cast<double2 *>(&sm.col[J0T + 2 * bi2]) = make_double2(c0, c1);
     }
     __syncthreads();
     const double dj = sm.col[j];
@@ -258,7 +322,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
       if (j == k - 2 && lane == 0) {
         sm.tq[j + 1][1] = sm.col[j + 1];
       }
-      continue;
+      return;
     }
     const double x = (lane > j + 1 && lane < k) ? sm.col[lane] : 0.0;
     const double alpha = sm.col[j + 1];
@@ -268,15 +332,16 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     double tau = 0.0, beta = alpha, scal = 0.0;
     if (xn2 > 0.0) {  // dlarfg, with fp64 rcp/rsq refined to ~1 ulp
       const double a2 = fma(alpha, alpha, xn2);
-      beta = -copysign(a2 * rsq64(a2), alpha);
-      tau = (beta - alpha) * rcp64(beta);
+      const double r = rsq64(a2);             // 1/|beta|
+      beta = -copysign(a2 * r, alpha);
+      tau = (beta - alpha) * -copysign(r, alpha);  // (beta - alpha) / beta
       scal = rcp64(alpha - beta);
     }
     if (lane == 0) {
       sm.tq[j + 1][1] = beta;
       sm.tau[j] = tau;
     }
-    if (tau == 0.0) continue;  // H_j = I (uniform)
+    if (tau == 0.0) return;  // H_j = I (uniform)
     // v_i = x_i * scal (i > j+1), v_{j+1} = 1, 0 elsewhere
     const double v = lane == j + 1 ? 1.0 : x * scal;
     if (lane < KP) sm.vb[lane] = v;
@@ -287,72 +352,120 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     ub = fma(-tau * s3, v, ub);
     __syncthreads();
     // partials of A v (block rows >= J only: v vanishes above)
-    double *pb = &sm.u.reg[SM::pb_base(J)] - J * SM::PLD;  // pb[R * PLD + col], R >= J
     double s1p = 0.0;  // this lane's share of v^T A v
-#pragma unroll
-    for (int it = 0; it < NBL; ++it) {
-      if (lane + 64 * it < NBLK && bi[it] >= J) {
-        double vi[4], vj[4];
-        ld4(&sm.vb[4 * bi[it]], vi);
-        ld4(&sm.vb[4 * bj[it]], vj);
-        double pr[4], pc[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pr[r] = acc[it][4 * r] * vj[0];
-#pragma unroll
-          for (int q = 1; q < 4; ++q) pr[r] = fma(acc[it][4 * r + q], vj[q], pr[r]);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          pc[q] = acc[it][q] * vi[0];
-#pragma unroll
-          for (int r = 1; r < 4; ++r) pc[q] = fma(acc[it][4 * r + q], vi[r], pc[q]);
-        }
-        double sp = vi[0] * pr[0];
-#pragma unroll
-        for (int r = 1; r < 4; ++r) sp = fma(vi[r], pr[r], sp);
-        double *dst = pb + bi[it] * SM::PLD + 4 * bj[it];
-        *reinterpret_cast<double2 *>(dst) = make_double2(pr[0], pr[1]);
-        *reinterpret_cast<double2 *>(dst + 2) = make_double2(pr[2], pr[3]);
-        if (bi[it] != bj[it]) {
-          if (bj[it] >= J) {
-            double *dt = pb + bj[it] * SM::PLD + 4 * bi[it];
-            *reinterpret_cast<double2 *>(dt) = make_double2(pc[0], pc[1]);
-            *reinterpret_cast<double2 *>(dt + 2) = make_double2(pc[2], pc[3]);
-          }
-          sp = sp + sp;  // the transposed block contributes v_j^T B^T v_i = v_i^T B v_j
-        }
-        s1p += sp;
-      }
-    }
-    const double s1 = tau * wave_sum_dpp(s1p);  // p . v with p = tau A v
-    __syncthreads();
     double pp = 0.0;
-    if (lane < KP && lane > j) {
-      const double *prow = pb + (lane >> 2) * SM::PLD + (lane & 3);
+    if constexpr (!ph2) {
+      double *pb = &sm.u.reg[SM::pb_base(J)] - J * SM::PLD;  // pb[R * PLD + col], R >= J
 #pragma unroll
-      for (int cb = 0; cb < SM::NB; ++cb) pp += prow[4 * cb];
+      for (int it = 0; it < NBL; ++it) {
+        if (lane + 64 * it < NBLK && bi[it] >= J) {
+          double vi[4], vj[4];
+          ld4(&sm.vb[4 * bi[it]], vi);
+          ld4(&sm.vb[4 * bj[it]], vj);
+          double pr[4], pc[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            pr[r] = A[it][4 * r] * vj[0];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) pr[r] = fma(A[it][4 * r + q], vj[q], pr[r]);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            pc[q] = A[it][q] * vi[0];
+#pragma unroll
+            for (int r = 1; r < 4; ++r) pc[q] = fma(A[it][4 * r + q], vi[r], pc[q]);
+          }
+          double sp = vi[0] * pr[0];
+#pragma unroll
+          for (int r = 1; r < 4; ++r) sp = fma(vi[r], pr[r], sp);
+          double *dst = pb + bi[it] * SM::PLD + 4 * bj[it];
+          *reinterpret_cast<double2 *>(dst) = make_double2(pr[0], pr[1]);
+          *reinterpret_cast<double2 *>(dst + 2) = make_double2(pr[2], pr[3]);
+          if (bi[it] != bj[it]) {
+            if (bj[it] >= J) {
+              double *dt = pb + bj[it] * SM::PLD + 4 * bi[it];
+              *reinterpret_cast<double2 *>(dt) = make_double2(pc[0], pc[1]);
+              *reinterpret_cast<double2 *>(dt + 2) = make_double2(pc[2], pc[3]);
+            }
+            sp = sp + sp;  // the transposed block contributes v_j^T B^T v_i = v_i^T B v_j
+          }
+          s1p += sp;
+        }
+      }
+      const double s1 = tau * wave_sum_dpp(s1p);  // p . v with p = tau A v
+      __syncthreads();
+      if (lane < KP && lane > j) {
+        const double *prow = pb + (lane >> 2) * SM::PLD + (lane & 3);
+        pp = prow[0];
+#pragma unroll
+        for (int cb = 1; cb < SM::NB; ++cb) pp += prow[4 * cb];
+      }
+      s1p = s1;
+    } else {
+      double *pb = &sm.u.reg[SM::pb2_base(J2)] - J2 * PLD2;  // pb[R * PLD2 + col], R >= J2
+      if (tail_lane && bi2 >= J2) {
+        const double2 vi = *reinterpret_cast<const double2 *>(&sm.vb[J0T + 2 * bi2]);
+        const double2 vj = *reinterpret_cast<const double2 *>(&sm.vb[J0T + 2 * bj2]);
+        const double pr0 = fma(A[0][1], vj.y, A[0][0] * vj.x);
+        const double pr1 = fma(A[0][3], vj.y, A[0][2] * vj.x);
+        double sp = fma(vi.y, pr1, vi.x * pr0);
+        *reinterpret_cast<double2 *>(pb + bi2 * PLD2 + 2 * bj2) = make_double2(pr0, pr1);
+        if (bi2 != bj2) {
+          if (bj2 >= J2) {
+            const double pc0 = fma(A[0][2], vi.y, A[0][0] * vi.x);
+            const double pc1 = fma(A[0][3], vi.y, A[0][1] * vi.x);
+            *reinterpret_cast<double2 *>(pb + bj2 * PLD2 + 2 * bi2) = make_double2(pc0, pc1);
+          }
+          sp = sp + sp;
+        }
+        s1p = sp;
+      }
+      const double s1 = tau * wave_sum_dpp(s1p);
+      __syncthreads();
+      if (lane < KP && lane > j) {
+        const double *prow = pb + ((lane - J0T) >> 1) * PLD2 + ((lane - J0T) & 1);
+        pp = prow[0];
+#pragma unroll
+        for (int cb = 1; cb < NB2; ++cb) pp += prow[2 * cb];
+      }
+      s1p = s1;
     }
+    const double s1 = s1p;
     const double p = (lane > j && lane < k) ? tau * pp : 0.0;
     const double w = fma(-0.5 * tau * s1, v, p);  // w = p - (tau/2)(p.v) v
     if (lane < KP) sm.wb[lane] = w;
     __syncthreads();
     // A <- A - v w^T - w v^T (rows and columns <= j are untouched: v, w vanish there)
+    if constexpr (!ph2) {
 #pragma unroll
-    for (int it = 0; it < NBL; ++it) {
-      if (lane + 64 * it < NBLK && bi[it] >= J) {
-        double vi[4], vj[4], wi[4], wj[4];
-        ld4(&sm.vb[4 * bi[it]], vi);
-        ld4(&sm.vb[4 * bj[it]], vj);
-        ld4(&sm.wb[4 * bi[it]], wi);
-        ld4(&sm.wb[4 * bj[it]], wj);
+      for (int it = 0; it < NBL; ++it) {
+        if (lane + 64 * it < NBLK && bi[it] >= J) {
+          double vi[4], vj[4], wi[4], wj[4];
+          ld4(&sm.vb[4 * bi[it]], vi);
+          ld4(&sm.vb[4 * bj[it]], vj);
+          ld4(&sm.wb[4 * bi[it]], wi);
+          ld4(&sm.wb[4 * bj[it]], wj);
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+          for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            acc[it][4 * r + q] = fma(-vi[r], wj[q], fma(-wi[r], vj[q], acc[it][4 * r + q]));
+            for (int q = 0; q < 4; ++q)
+              A[it][4 * r + q] = fma(-vi[r], wj[q], fma(-wi[r], vj[q], A[it][4 * r + q]));
+        }
       }
+    } else if (tail_lane && bi2 >= J2) {
+      const double2 vi = *reinterpret_cast<const double2 *>(&sm.vb[J0T + 2 * bi2]);
+      const double2 vj = *reinterpret_cast<const double2 *>(&sm.vb[J0T + 2 * bj2]);
+      const double2 wi = *reinterpret_cast<const double2 *>(&sm.wb[J0T + 2 * bi2]);
+      const double2 wj = *reinterpret_cast<const double2 *>(&sm.wb[J0T + 2 * bj2]);
+      A[0][0] = fma(-vi.x, wj.x, fma(-wi.x, vj.x, A[0][0]));
+      A[0][1] = fma(-vi.x, wj.y, fma(-wi.x, vj.y, A[0][1]));
+      A[0][2] = fma(-vi.y, wj.x, fma(-wi.y, vj.x, A[0][2]));
+      A[0][3] = fma(-vi.y, wj.y, fma(-wi.y, vj.y, A[0][3]));
     }
+  };
+  for (int j = 0; j < (k < J0T ? k : J0T); ++j) step(j, std::false_type{}, acc);
+  if constexpr (J0T < KP) {
+    for (int j = J0T; j < k; ++j) step(j, std::true_type{}, acc);
   }
   // after the Householder vectors (the partials are dead): per side, in walk order, the
   // quadrature sum (Ym) and node 31's exact solve (Zm)

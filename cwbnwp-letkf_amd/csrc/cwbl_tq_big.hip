@@ -211,8 +211,9 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     double tau = 0.0, beta = alpha, scal = 0.0;
     if (xn2 > 0.0) {  // dlarfg, fp64 rcp/rsq refined to ~1 ulp
       const double a2 = fma(alpha, alpha, xn2);
-      beta = -copysign(a2 * rsq64(a2), alpha);
-      tau = (beta - alpha) * rcp64(beta);
+      const double r = rsq64(a2);             // 1/|beta|
+      beta = -copysign(a2 * r, alpha);
+      tau = (beta - alpha) * -copysign(r, alpha);  // (beta - alpha) / beta
       scal = rcp64(alpha - beta);
     }
     if (tid == 0) {
