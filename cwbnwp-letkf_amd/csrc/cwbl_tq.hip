@@ -259,13 +259,15 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   // register assignment (one loop with a run-time phase test copies the blocks between
   // registers every step).  The blocks are reached through the capture at NBL = 1 and
   // through the parameter otherwise: the other way round, the compiler keeps them in scratch.
-  auto step = [&](const int j, auto phase, double (&Ap)[NBL][16]) __attribute__((always_inline)) {
+  auto step = [&](const int j, auto phase, auto q, double (&Ap)[NBL][16])
+                  __attribute__((always_inline)) {
     constexpr bool ph2 = decltype(phase)::value;
+    constexpr int qj = decltype(q)::value, q2 = qj;  // column within the block: constant
     double (&A)[NBL][16] = *[&]() {
       if constexpr (NBL == 1) return &acc; else return &Ap;
     }();
-    const int J = j >> 2, qj = j & 3;
-    const int J2 = (j - J0T) >> 1, q2 = (j - J0T) & 1;
+    const int J = j >> 2;
+    const int J2 = (j - J0T) >> 1;
     if constexpr (ph2) {
       if (j == J0T) {  // re-deal the tail: 4x4 blocks -> packed lower triangle -> 2x2 blocks
         double *tri = &sm.u.reg[J0T < KP ? SM::pb2_base(0) : 0];
@@ -299,19 +301,14 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
 #pragma unroll
       for (int it = 0; it < NBL; ++it) {
         if (lane + 64 * it < NBLK && bj[it] == J) {  // publish column j
-          double cv[4];
-          switch (qj) {
-            case 0: for (int r = 0; r < 4; ++r) cv[r] = A[it][4 * r]; break;
-            case 1: for (int r = 0; r < 4; ++r) cv[r] = A[it][4 * r + 1]; break;
-            case 2: for (int r = 0; r < 4; ++r) cv[r] = A[it][4 * r + 2]; break;
-            default: for (int r = 0; r < 4; ++r) cv[r] = A[it][4 * r + 3]; break;
-          }
-          *reinterpret_cast<double2 *>(&sm.col[4 * bi[it]]) = make_double2(cv[0], cv[1]);
-          *reinterpret_cast<double2 *>(&sm.col[4 * bi[it] + 2]) = make_double2(cv[2], cv[3]);
+          *reinterpret_cast<double2 *>(&sm.col[4 * bi[it]]) =
+              make_double2(A[it][qj], A[it][4 + qj]);
+          *reinterpret_cast<double2 *>(&sm.col[4 * bi[it] + 2]) =
+              make_double2(A[it][8 + qj], A[it][12 + qj]);
         }
       }
     } else if (tail_lane && bj2 == J2) {  // publish column j (2x2 phase)
-      const double c0 = q2 ? A[0][1] : A[0][0], c1 = q2 ? A[0][3] : A[0][2];
+      const double c0 = A[0][q2 & 1], c1 = A[0][2 + (q2 & 1)];
       *reinterpret_cast<double2 *>(&sm.col[J0T + 2 * bi2]) = make_double2(c0, c1);
     }
     __syncthreads();
@@ -463,9 +460,21 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
       A[0][3] = fma(-vi.y, wj.y, fma(-wi.y, vj.y, A[0][3]));
     }
   };
-  for (int j = 0; j < (k < J0T ? k : J0T); ++j) step(j, std::false_type{}, acc);
+  // unrolled by the block width, so that the pivot column's registers are known statically
+  using std::false_type, std::true_type, std::integral_constant;
+  const int jend1 = k < J0T ? k : J0T;
+  for (int j = 0; j < jend1; j += 4) {
+    step(j, false_type{}, integral_constant<int, 0>{}, acc);
+    if (j + 1 < jend1) step(j + 1, false_type{}, integral_constant<int, 1>{}, acc);
+    if (j + 2 < jend1) step(j + 2, false_type{}, integral_constant<int, 2>{}, acc);
+    if (j + 3 < jend1) step(j + 3, false_type{}, integral_constant<int, 3>{}, acc);
+  }
   if constexpr (J0T < KP) {
-    for (int j = J0T; j < k; ++j) step(j, std::true_type{}, acc);
+    static_assert(J0T % 2 == 0, "2x2 phase alignment");
+    for (int j = J0T; j < k; j += 2) {
+      step(j, true_type{}, integral_constant<int, 0>{}, acc);
+      if (j + 1 < k) step(j + 1, true_type{}, integral_constant<int, 1>{}, acc);
+    }
   }
   // after the Householder vectors (the partials are dead): per side, in walk order, the
   // quadrature sum (Ym) and node 31's exact solve (Zm)
