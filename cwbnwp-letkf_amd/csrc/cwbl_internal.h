@@ -141,6 +141,18 @@ hipError_t launch_solve_tq(hipStream_t s, int kp, bool assembled, const TreeDesc
                            const long long *col_off, const float *yo, const float *yb,
                            const float *xb, float *xa, int2 *info);
 
+// Split form of the KP = 40 slab path: solve_tq_kernel stops after the assembly and hands
+// A (packed lower, KP(KP+1)/2 fp64 per point) and Yb d (KP fp64) over through the workspace
+// (info[gi] = (p, 0)); solve_tq4_kernel (cwbl_tq4.hip, four points per wavefront) finishes
+// the solve and writes var in place.  kTq4KP is the only KP both are instantiated for.
+constexpr int kTq4KP = 40;
+hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
+                                   SlabDev slab, long long g0, int npts, const int *nbr_cnt,
+                                   const int *nbr_idx, int2 *info, double *ws_a,
+                                   double *ws_b1);
+hipError_t launch_solve_tq4(hipStream_t s, int kp, SolveConsts c, SlabDev slab, long long g0,
+                            int npts, const double *ws_a, const double *ws_b1, int2 *info);
+
 // KP = 96, 128: one 256-thread workgroup per point (cwbl_tq_big.hip)
 hipError_t launch_solve_tq_big(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,
                                SolveConsts c, SlabDev slab, long long g0, int npts,

@@ -98,14 +98,17 @@ struct TqOccupancy {
   static constexpr int kWaves = KP <= 40 ? 4 : KP <= 48 ? 3 : 2;
 };
 
-template <int KP, bool ASSEMBLED>
+// HANDOFF: stop after the assembly and hand A = inflat I + Yb Yb^T (packed lower, fp64) and
+// Yb d to solve_tq4_kernel (cwbl_tq4.hip) through ws_a / ws_b1; info[gi] = (p, 0).
+template <int KP, bool ASSEMBLED, bool HANDOFF = false>
 __global__ void __launch_bounds__(64, TqOccupancy<KP>::kWaves)
 solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, long long g0,
                 int npts, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
                 const long long *__restrict__ col_off,
                 const float *__restrict__ yo_in, const float *__restrict__ yb_in,
                 const float *__restrict__ xb_in, float *__restrict__ xa_out,
-                int2 *__restrict__ info) {
+                int2 *__restrict__ info, double *__restrict__ ws_a = nullptr,
+                double *__restrict__ ws_b1 = nullptr) {
   static_assert(KP % 8 == 0 && KP <= 64, "KP");
   constexpr int H = KP / 2;
   constexpr int NBL = AsmLayout<KP>::NBL, NBLK = AsmLayout<KP>::NBLK;
@@ -173,6 +176,31 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
 #pragma unroll
       for (int q = 0; q < MfmaLayout<KP>::NTL; ++q) t += tile[q][0] + tile[q][3];
       if (lane == 0 && info) info[gi] = make_int2(ptot, (int)t);
+      return;
+    }
+    if constexpr (HANDOFF) {  // A and Yb d to the workspace, rows of A packed lower
+      using ML = MfmaLayout<KP>;
+      constexpr int NA = KP * (KP + 1) / 2;
+      double *__restrict__ aw = ws_a + (long long)gi * NA;
+      double *__restrict__ bw = ws_b1 + (long long)gi * KP;
+      const double inflat_r8 = (double)c.inflat;
+      int t = 0;
+#pragma unroll
+      for (int I = 0; I < ML::NT; ++I)
+#pragma unroll
+        for (int J = 0; J <= I; ++J, ++t) {
+          const int col = 16 * J + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * I + (lane >> 4) + 4 * r;
+            double v = tile[t][r];
+            if (row == col) v = row < k ? v + inflat_r8 : 1.0;  // padding rows: identity
+            if (row < KP && col <= row) aw[row * (row + 1) / 2 + col] = v;
+            if (ML::YO_ROW && row == KP && col < KP) bw[col] = v;
+          }
+        }
+      if (!ML::YO_ROW && lane < KP) bw[lane] = b1acc;
+      if (lane == 0) info[gi] = make_int2(ptot, 0);
       return;
     }
     // MFMA tiles -> LDS (two row halves) -> 4x4 register blocks
@@ -619,6 +647,31 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   }
   // info.y: decade of the quadrature rule (negative when M/m exceeds the last table)
   if (lane == 0 && info) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
+}
+
+template <int KP>
+static hipError_t launch_tq_handoff_kp(hipStream_t s, const TreeDesc *trees, SolveConsts c,
+                                       SlabDev slab, long long g0, int npts,
+                                       const int *nbr_cnt, const int *nbr_idx, int2 *info,
+                                       double *ws_a, double *ws_b1) {
+  hipLaunchKernelGGL((solve_tq_kernel<KP, false, true>), dim3(npts), dim3(64), 0, s, trees, c,
+                     slab, g0, npts, nbr_cnt, nbr_idx, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, info, ws_a, ws_b1);
+  return hipGetLastError();
+}
+
+hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
+                                   SlabDev slab, long long g0, int npts, const int *nbr_cnt,
+                                   const int *nbr_idx, int2 *info, double *ws_a,
+                                   double *ws_b1) {
+  if (npts <= 0) return hipSuccess;
+  switch (kp) {
+    case 40:
+      return launch_tq_handoff_kp<40>(s, trees, c, slab, g0, npts, nbr_cnt, nbr_idx, info,
+                                      ws_a, ws_b1);
+    default:
+      return hipErrorInvalidValue;
+  }
 }
 
 template <int KP>
