@@ -180,14 +180,17 @@ def main():
         flops = synth.flops_total(k, solved, nobs_sum)
         achieved = flops / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else 0.0
         kp = ((k + 7) // 8) * 8 if k <= 64 else (96 if k <= 96 else 128)
-        kname = ("solve_kernel" if jacobi else
-                 "solve_tq_kernel" if kp <= 64 else "solve_tq_big_kernel") + f"<{kp}, false>"
+        split = (not jacobi and kp == 40 and os.environ.get("CWBL_TQ4", "1") != "0")
+        kname = ("solve_tq_kernel<40, false, 8> + solve_tq4_kernel<40, 8>" if split else
+                 ("solve_kernel" if jacobi else
+                  "solve_tq_kernel" if kp <= 64 else "solve_tq_big_kernel") + f"<{kp}, false>")
         traffic = None  # HBM bytes per launch from the committed PMC pass of this kernel
         pmc = os.path.join(REPO, "profiles", "pmc_solve_traffic.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 pm = json.load(f)
-            if pm.get("kernel", "").endswith(kname) and args.config == pm.get("config", "c2"):
+            if pm.get("kernel", "").replace("void ", "").replace("cwbl::", "") == kname and \
+                    args.config == pm.get("config", "c2"):
                 traffic = pm.get("hbm_bytes_per_launch")
         out = {
             "metric": METRIC,
@@ -220,7 +223,8 @@ def main():
                 "frac": achieved / FP64_PEAK_TFLOPS,
                 "traffic": traffic,
                 "kernel": kname,
-                "note": "FP64 flops F(k,p) of SURVEY.md 8(d) per solve launch / HIP-event launch time (rank 0)",
+                "note": "FP64 flops F(k,p) of SURVEY.md 8(d) per batch / HIP-event time of the batch's "
+                        "solve launches (rank 0); traffic: PMC HBM bytes of those launches",
             },
             "detail": {
                 "solver": "jacobi" if jacobi else "householder+quadrature",

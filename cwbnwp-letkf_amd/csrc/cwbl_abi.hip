@@ -102,9 +102,9 @@ struct State {
   DevBuf bcol, byo, byb, bxb, bxa, bev;               // solve_batch staging
   DevBuf qxyz, qnf, qidx, qr2;                        // search staging
   DevBuf quad;                                        // x^-1/2 quadrature tables
-  DevBuf wsa, wsb1;                                   // A / Yb d hand-off (split KP=40 path)
+  DevBuf wsa;                                         // hand-off records (split KP=40 path)
   bool jacobi = false;                                // CWBL_SOLVER=jacobi: eigen path
-  bool tq4 = false;                                   // CWBL_TQ4=1: split KP=40 solve (tq4)
+  bool tq4 = true;                                    // CWBL_TQ4=0: one-kernel KP=40 solve
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: hand-off batch (points)
   std::vector<hipEvent_t> events;
 };
@@ -287,7 +287,7 @@ void release_all() {
   release_obs();
   for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.info, &S.stats, &S.sx,
                     &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev,
-                    &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad, &S.wsa, &S.wsb1})
+                    &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad, &S.wsa})
     b->release();
   for (hipEvent_t e : S.events) (void)hipEventDestroy(e);
   S.events.clear();
@@ -365,7 +365,7 @@ int cwbl_init(const cwbl_init_params *p) {
   }
   const char *solver = std::getenv("CWBL_SOLVER");
   S.jacobi = solver && std::strcmp(solver, "jacobi") == 0;
-  S.tq4 = false;
+  S.tq4 = true;
   if (const char *e = std::getenv("CWBL_TQ4")) S.tq4 = std::atoi(e) != 0;
   if (const char *e = std::getenv("CWBL_TQ4_SUB")) S.tq4_sub = std::atoll(e);
   S.inited = true;
@@ -542,18 +542,15 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       // points (a multiple of kListLanes, so a batch's neighbour lists start on a group)
       long long Bs = S.tq4_sub > 0 ? S.tq4_sub : nb;
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
-      const size_t na = (size_t)kTq4KP * (kTq4KP + 1) / 2;
-      HIPCHK(S.wsa.ensure((size_t)Bs * na * 8));
-      HIPCHK(S.wsb1.ensure((size_t)Bs * kTq4KP * 8));
+      HIPCHK(S.wsa.ensure((size_t)Bs * Tq4Handoff<kTq4KP, kTq4J0>::WORDS * 8));
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
         const int ns = (int)std::min<long long>(Bs, nb - s0);
         HIPCHK(launch_assemble_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
                                        S.nbr_cnt.as<int>() + s0 * nt,
                                        S.nbr_idx.as<int>() + s0 * list_cap,
-                                       S.info.as<int2>() + s0, S.wsa.as<double>(),
-                                       S.wsb1.as<double>()));
+                                       S.info.as<int2>() + s0, S.wsa.as<double>()));
         HIPCHK(launch_solve_tq4(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
-                                S.wsb1.as<double>(), S.info.as<int2>() + s0));
+                                S.info.as<int2>() + s0));
       }
     } else
       HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, S.nbr_cnt.as<int>(),

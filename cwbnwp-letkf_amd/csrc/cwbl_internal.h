@@ -141,17 +141,31 @@ hipError_t launch_solve_tq(hipStream_t s, int kp, bool assembled, const TreeDesc
                            const long long *col_off, const float *yo, const float *yb,
                            const float *xb, float *xa, int2 *info);
 
-// Split form of the KP = 40 slab path: solve_tq_kernel stops after the assembly and hands
-// A (packed lower, KP(KP+1)/2 fp64 per point) and Yb d (KP fp64) over through the workspace
-// (info[gi] = (p, 0)); solve_tq4_kernel (cwbl_tq4.hip, four points per wavefront) finishes
-// the solve and writes var in place.  kTq4KP is the only KP both are instantiated for.
+// Split form of the KP = 40 slab path: solve_tq_kernel<40, false, kTq4J0> assembles A and
+// runs the first kTq4J0 Householder steps (4x4 register blocks, one point per wavefront),
+// then hands the rest over through the workspace (Tq4Handoff, info[gi] = (p, 0));
+// solve_tq4_kernel (cwbl_tq4.hip) finishes the tridiagonalisation on the 32 x 32 trailing
+// matrix with four points per wavefront, solves and writes var in place.
 constexpr int kTq4KP = 40;
+constexpr int kTq4J0 = 8;
+// fp64 words of one point's hand-off record
+template <int KP, int J0>
+struct Tq4Handoff {
+  static constexpr int KT = KP - J0;            // trailing rows
+  static constexpr int NT = KT * (KT + 1) / 2;  // trailing A, packed lower (rows J0..KP-1)
+  static constexpr int HV = NT;                 // reflectors 0..J0-1 as KP-rows (0 above j+1)
+  static constexpr int D = HV + J0 * KP;        // d_0 .. d_{J0-1}
+  static constexpr int E = D + J0;              // c(j, j+1), j = 0..J0-1
+  static constexpr int TAU = E + J0;            // tau_0 .. tau_{J0-1}
+  static constexpr int U1 = TAU + J0;           // Q_J0^T b1 (KP)
+  static constexpr int U2 = U1 + KP;            // Q_J0^T x' (KP)
+  static constexpr int WORDS = (U2 + KP + 1) / 2 * 2;
+};
 hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
                                    SlabDev slab, long long g0, int npts, const int *nbr_cnt,
-                                   const int *nbr_idx, int2 *info, double *ws_a,
-                                   double *ws_b1);
+                                   const int *nbr_idx, int2 *info, double *ws);
 hipError_t launch_solve_tq4(hipStream_t s, int kp, SolveConsts c, SlabDev slab, long long g0,
-                            int npts, const double *ws_a, const double *ws_b1, int2 *info);
+                            int npts, const double *ws, int2 *info);
 
 // KP = 96, 128: one 256-thread workgroup per point (cwbl_tq_big.hip)
 hipError_t launch_solve_tq_big(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,

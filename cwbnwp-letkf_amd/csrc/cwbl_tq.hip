@@ -98,17 +98,17 @@ struct TqOccupancy {
   static constexpr int kWaves = KP <= 40 ? 4 : KP <= 48 ? 3 : 2;
 };
 
-// HANDOFF: stop after the assembly and hand A = inflat I + Yb Yb^T (packed lower, fp64) and
-// Yb d to solve_tq4_kernel (cwbl_tq4.hip) through ws_a / ws_b1; info[gi] = (p, 0).
-template <int KP, bool ASSEMBLED, bool HANDOFF = false>
+// HS > 0: after the assembly and the first HS Householder steps, hand the trailing matrix,
+// the reflectors, T so far and Q^T b1, Q^T x' over to solve_tq4_kernel (cwbl_tq4.hip)
+// through ws (Tq4Handoff); info[gi] = (p, 0).
+template <int KP, bool ASSEMBLED, int HS = 0>
 __global__ void __launch_bounds__(64, TqOccupancy<KP>::kWaves)
 solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, long long g0,
                 int npts, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
                 const long long *__restrict__ col_off,
                 const float *__restrict__ yo_in, const float *__restrict__ yb_in,
                 const float *__restrict__ xb_in, float *__restrict__ xa_out,
-                int2 *__restrict__ info, double *__restrict__ ws_a = nullptr,
-                double *__restrict__ ws_b1 = nullptr) {
+                int2 *__restrict__ info, double *__restrict__ ws = nullptr) {
   static_assert(KP % 8 == 0 && KP <= 64, "KP");
   constexpr int H = KP / 2;
   constexpr int NBL = AsmLayout<KP>::NBL, NBLK = AsmLayout<KP>::NBLK;
@@ -176,31 +176,6 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
 #pragma unroll
       for (int q = 0; q < MfmaLayout<KP>::NTL; ++q) t += tile[q][0] + tile[q][3];
       if (lane == 0 && info) info[gi] = make_int2(ptot, (int)t);
-      return;
-    }
-    if constexpr (HANDOFF) {  // A and Yb d to the workspace, rows of A packed lower
-      using ML = MfmaLayout<KP>;
-      constexpr int NA = KP * (KP + 1) / 2;
-      double *__restrict__ aw = ws_a + (long long)gi * NA;
-      double *__restrict__ bw = ws_b1 + (long long)gi * KP;
-      const double inflat_r8 = (double)c.inflat;
-      int t = 0;
-#pragma unroll
-      for (int I = 0; I < ML::NT; ++I)
-#pragma unroll
-        for (int J = 0; J <= I; ++J, ++t) {
-          const int col = 16 * J + (lane & 15);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = 16 * I + (lane >> 4) + 4 * r;
-            double v = tile[t][r];
-            if (row == col) v = row < k ? v + inflat_r8 : 1.0;  // padding rows: identity
-            if (row < KP && col <= row) aw[row * (row + 1) / 2 + col] = v;
-            if (ML::YO_ROW && row == KP && col < KP) bw[col] = v;
-          }
-        }
-      if (!ML::YO_ROW && lane < KP) bw[lane] = b1acc;
-      if (lane == 0) info[gi] = make_int2(ptot, 0);
       return;
     }
     // MFMA tiles -> LDS (two row halves) -> 4x4 register blocks
@@ -490,12 +465,48 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   };
   // unrolled by the block width, so that the pivot column's registers are known statically
   using std::false_type, std::true_type, std::integral_constant;
-  const int jend1 = k < J0T ? k : J0T;
+  const int jend1 = HS > 0 ? (k < HS ? k : HS) : (k < J0T ? k : J0T);
   for (int j = 0; j < jend1; j += 4) {
     step(j, false_type{}, integral_constant<int, 0>{}, acc);
     if (j + 1 < jend1) step(j + 1, false_type{}, integral_constant<int, 1>{}, acc);
     if (j + 2 < jend1) step(j + 2, false_type{}, integral_constant<int, 2>{}, acc);
     if (j + 3 < jend1) step(j + 3, false_type{}, integral_constant<int, 3>{}, acc);
+  }
+  if constexpr (HS > 0) {  // hand-off (Tq4Handoff) after HS steps
+    static_assert(HS % 4 == 0 && HS <= J0T, "hand-off at a block boundary");
+    using HO = Tq4Handoff<KP, HS>;
+    double *__restrict__ w = ws + (long long)gi * HO::WORDS;
+    constexpr int JB = HS / 4;
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) {  // trailing blocks, packed lower
+      if (lane + 64 * it < NBLK && bj[it] >= JB) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int a = 4 * (bi[it] - JB) + r, b = 4 * (bj[it] - JB) + q;
+            if (a >= b) w[a * (a + 1) / 2 + b] = acc[it][4 * r + q];
+          }
+      }
+    }
+    __syncthreads();
+    if (lane < KP) {
+      for (int j = 0; j < HS; ++j) {  // reflector j (never stored when tau = 0: H = I)
+        const double t = sm.tau[j];
+        const int off = j * (k - 1) - j * (j - 1) / 2 + lane - (j + 1);
+        w[HO::HV + j * KP + lane] =
+            (t != 0.0 && lane > j && lane < k) ? sm.u.reg[SM::hv_off(0) + off] : 0.0;
+      }
+      w[HO::U1 + lane] = ub;
+      w[HO::U2 + lane] = ux;
+    }
+    if (lane < HS) {
+      w[HO::D + lane] = sm.tq[lane][0];
+      w[HO::E + lane] = sm.tq[lane + 1][1];
+      w[HO::TAU + lane] = sm.tau[lane];
+    }
+    if (lane == 0) info[gi] = make_int2(ptot, 0);
+    return;
   }
   if constexpr (J0T < KP) {
     static_assert(J0T % 2 == 0, "2x2 phase alignment");
@@ -649,29 +660,15 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   if (lane == 0 && info) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
 }
 
-template <int KP>
-static hipError_t launch_tq_handoff_kp(hipStream_t s, const TreeDesc *trees, SolveConsts c,
-                                       SlabDev slab, long long g0, int npts,
-                                       const int *nbr_cnt, const int *nbr_idx, int2 *info,
-                                       double *ws_a, double *ws_b1) {
-  hipLaunchKernelGGL((solve_tq_kernel<KP, false, true>), dim3(npts), dim3(64), 0, s, trees, c,
-                     slab, g0, npts, nbr_cnt, nbr_idx, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, info, ws_a, ws_b1);
-  return hipGetLastError();
-}
-
 hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
                                    SlabDev slab, long long g0, int npts, const int *nbr_cnt,
-                                   const int *nbr_idx, int2 *info, double *ws_a,
-                                   double *ws_b1) {
+                                   const int *nbr_idx, int2 *info, double *ws) {
   if (npts <= 0) return hipSuccess;
-  switch (kp) {
-    case 40:
-      return launch_tq_handoff_kp<40>(s, trees, c, slab, g0, npts, nbr_cnt, nbr_idx, info,
-                                      ws_a, ws_b1);
-    default:
-      return hipErrorInvalidValue;
-  }
+  if (kp != kTq4KP) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((solve_tq_kernel<kTq4KP, false, kTq4J0>), dim3(npts), dim3(64), 0, s,
+                     trees, c, slab, g0, npts, nbr_cnt, nbr_idx, nullptr, nullptr, nullptr,
+                     nullptr, nullptr, info, ws);
+  return hipGetLastError();
 }
 
 template <int KP>

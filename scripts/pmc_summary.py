@@ -39,15 +39,21 @@ def main(src, tag):
             e["hbm_bytes_per_launch_corrected"] = (2 * fetch[k] + (write.get(k) or 0)) * 1024
         out["kernels"][k] = e
     names = list(out["kernels"])
-    solve = ([k for k in names if "solve_tq_kernel" in k] or [k for k in names if "solve_kernel" in k])[0]
+    # the solve: the split KP=40 pair (assembly + 8 steps, then solve_tq4_kernel), one
+    # launch of each per batch, or the single solve kernel
+    solve = [k for k in names if "solve_tq_kernel" in k or "solve_tq4_kernel" in k] or \
+        [k for k in names if "solve_kernel" in k]
+    short = lambda k: k.replace("void ", "").replace("cwbl::", "")  # noqa: E731
     os.makedirs("profiles", exist_ok=True)
     import shutil
     shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), f"profiles/{tag}_kernel_stats.csv")
     json.dump(out, open(f"profiles/{tag}_summary.json", "w"), indent=1)
-    json.dump({"kernel": solve, "tag": tag,
-               "hbm_bytes_per_launch": out["kernels"][solve]["hbm_bytes_per_launch_corrected"],
-               "avg_launch_ms": out["kernels"][solve]["avg_ms"],
-               "note": "(2*FETCH_SIZE + WRITE_SIZE) KiB x 1024, separate rocprofv3 --pmc passes"},
+    json.dump({"kernel": " + ".join(short(k) for k in solve), "tag": tag,
+               "hbm_bytes_per_launch": sum(out["kernels"][k]["hbm_bytes_per_launch_corrected"]
+                                           for k in solve),
+               "avg_launch_ms": sum(out["kernels"][k]["avg_ms"] for k in solve),
+               "note": "(2*FETCH_SIZE + WRITE_SIZE) KiB x 1024, separate rocprofv3 --pmc passes; "
+                       "per batch, summed over the solve kernels"},
               open("profiles/pmc_solve_traffic.json", "w"), indent=1)
     print(json.dumps(out, indent=1))
 
