@@ -540,8 +540,13 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     else if (S.tq4 && S.kp == kTq4KP) {
       // assembly -> workspace -> four-points-per-wave solve, in hand-off batches of Bs
       // points (a multiple of kListLanes, so a batch's neighbour lists start on a group)
-      long long Bs = S.tq4_sub > 0 ? S.tq4_sub : nb;
+      // (Bs <= 2^19: the solve addresses a batch's records with 32-bit byte offsets), the
+      // search batch split evenly
+      const long long cap = std::min<long long>(S.tq4_sub > 0 ? S.tq4_sub : nb, 1 << 19);
+      const long long nsub = (nb + cap - 1) / cap;
+      long long Bs = (nb + nsub - 1) / nsub;
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
+      Bs = std::min<long long>(Bs, 1 << 19);
       HIPCHK(S.wsa.ensure((size_t)Bs * Tq4Handoff<kTq4KP, kTq4J0>::WORDS * 8));
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
         const int ns = (int)std::min<long long>(Bs, nb - s0);

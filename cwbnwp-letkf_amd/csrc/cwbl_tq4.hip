@@ -87,7 +87,10 @@ solve_tq4_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   const bool valid = gi < npts;
   const int k = c.k;
   const int ptot = valid ? info[gi].x : 0;
-  const double *__restrict__ w = ws + (long long)(valid ? gi : 0) * HO::WORDS;
+  // hand-off words of this point: ws[wb + i] through an SGPR base and a 32-bit VGPR
+  // offset (the host keeps a hand-off batch below 2^32 bytes)
+  const unsigned wb = (unsigned)(valid ? gi : 0) * (unsigned)HO::WORDS;
+  auto w = [&](int i) { return gld(ws, wb + (unsigned)i); };
   // global row of vector slot vs (rows that do not exist get KP + 1: never < k)
   auto vrow = [&](int vs) { return vs == 0 ? (l < J0 ? l : KP + 1) : J0 + l + 16 * (vs - 1); };
 
@@ -107,50 +110,30 @@ solve_tq4_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     const int t = l + 16 * r;
     sfor<KT>([&](auto cc) {
       constexpr int col = decltype(cc)::value;
-      A[r][col] = w[col <= t ? t * (t + 1) / 2 + col : col * (col + 1) / 2 + t];
+      A[r][col] = w(col <= t ? t * (t + 1) / 2 + col : col * (col + 1) / 2 + t);
     });
   });
 
-  // ---- background of the point: member i = row i ------------------------------------------
-  float xbl[NV];
-  sfor<NV>([&](auto vv) {
-    constexpr int vs = decltype(vv)::value;
-    const int i = vrow(vs);
-    xbl[vs] = (valid && i < k) ? slab.var[P + slab.L * i] : 0.0f;
-  });
-  // fp32 sum over members in member order; member m is row m: prefix slot lane m (m < J0),
-  // else trailing slot (m - J0) / 16, lane (m - J0) % 16
-  auto seq_sum_f32 = [&](const float (&x)[NV]) {
-    float s = 0.0f;
-    sfor<KP>([&](auto mm) {
-      constexpr int m = decltype(mm)::value;
-      constexpr int vs = m < J0 ? 0 : 1 + (m - J0) / 16, ln = m < J0 ? m : (m - J0) % 16;
-      const float b = rbcast<ln>(x[vs]);
-      s = s + (m < k ? b : 0.0f);  // s + 0 = s: s is never -0
-    });
-    return s;
-  };
-  // sum(xb) * nmember_inv (:671)
-  const double xb_mean = (double)(seq_sum_f32(xbl) * c.nmember_inv);
   double ux[NS], ub[NS];  // trailing rows of Q^T x' and Q^T b1
   sfor<NS>([&](auto rr) {
     constexpr int r = decltype(rr)::value;
     const int t = J0 + l + 16 * r;
-    ux[r] = w[HO::U2 + t];
-    ub[r] = w[HO::U1 + t];
+    ux[r] = w(HO::U2 + t);
+    ub[r] = w(HO::U1 + t);
   });
   // T rows < J0 (and c(J0-1, J0)) and the first reflectors' tau, from the hand-off
-  if (l < J0) {
-    sm.tq[q][l][0] = w[HO::D + l];
-    sm.tq[q][l + 1][1] = w[HO::E + l];
-    sm.tq[q][l][2] = w[HO::U1 + l];
-    sm.tq[q][l][3] = w[HO::U2 + l];
-    sm.tau[q][l] = w[HO::TAU + l];
+  {
+    const int lj = l < J0 ? l : J0 - 1;  // lanes >= J0 repeat row J0-1 (same values)
+    sm.tq[q][lj][0] = w(HO::D + lj);
+    sm.tq[q][lj + 1][1] = w(HO::E + lj);
+    sm.tq[q][lj][2] = w(HO::U1 + lj);
+    sm.tq[q][lj][3] = w(HO::U2 + lj);
+    sm.tau[q][lj] = w(HO::TAU + lj);
   }
   double trace = 0.0;  // sum of d_j, j < k
   sfor<J0>([&](auto jj) {
     constexpr int j = decltype(jj)::value;
-    trace += j < k ? w[HO::D + j] : 0.0;
+    trace += j < k ? w(HO::D + j) : 0.0;
   });
 
   // ---- Householder steps J0 .. KP-3 on the trailing matrix (local column jl) --------------
@@ -336,7 +319,10 @@ solve_tq4_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     constexpr int vs = decltype(vv)::value;
     const int i = vrow(vs);
     double u1 = 0.0;
-    if constexpr (vs == 0) u1 = l < J0 ? w[HO::U1 + l] : 0.0;
+    if constexpr (vs == 0) {
+      const double t = w(HO::U1 + (l < J0 ? l : 0));
+      u1 = l < J0 ? t : 0.0;
+    }
     else u1 = ub[vs - 1];
     dpart = i < KP ? fma(u1, z[vs], dpart) : dpart;
   });
@@ -372,7 +358,8 @@ solve_tq4_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     sfor<NV>([&](auto vs_c) {
       constexpr int vs = decltype(vs_c)::value;
       const int i = vrow(vs);
-      vv[vs] = i < KP ? w[HO::HV + j * KP + i] : 0.0;
+      const double h = w(HO::HV + j * KP + (i < KP ? i : 0));  // branch-free load
+      vv[vs] = i < KP ? h : 0.0;
       a = fma(vv[vs], y[vs], a);
     });
     a = row16_sum(a);
@@ -382,6 +369,30 @@ solve_tq4_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     });
   });
 
+  // ---- background of the point: member i = row i (loaded here, where it is used: loaded
+  // early, the compiler keeps its 40 broadcasts live across the whole kernel) ------------
+  float xbl[NV];
+  sfor<NV>([&](auto vv) {
+    constexpr int vs = decltype(vv)::value;
+    const int i = vrow(vs);
+    const bool mem = valid && i < k;
+    const float xv = slab.var[P + slab.L * (mem ? i : 0)];  // branch-free: a valid address
+    xbl[vs] = mem ? xv : 0.0f;
+  });
+  // fp32 sum over members in member order; member m is row m: prefix slot lane m (m < J0),
+  // else trailing slot (m - J0) / 16, lane (m - J0) % 16
+  auto seq_sum_f32 = [&](const float (&x)[NV]) {
+    float s = 0.0f;
+    sfor<KP>([&](auto mm) {
+      constexpr int m = decltype(mm)::value;
+      constexpr int vs = m < J0 ? 0 : 1 + (m - J0) / 16, ln = m < J0 ? m : (m - J0) % 16;
+      const float b = rbcast<ln>(x[vs]);
+      s = s + (m < k ? b : 0.0f);  // s + 0 = s: s is never -0
+    });
+    return s;
+  };
+  // sum(xb) * nmember_inv (:671)
+  const double xb_mean = (double)(seq_sum_f32(xbl) * c.nmember_inv);
   // ---- analysis and RTPP / RTPS (:675-698), fp32 in the reference's order ----------------
   const double sk = sqrt((double)(k - 1));
   float xa[NV];
