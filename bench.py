@@ -101,6 +101,70 @@ def time_transposes(core, w, k, rank, world, dev):
     return res
 
 
+# input.nml's var_update (:7) and multi_infl (:162), with the slab each variable takes in
+# letkf_driver (module_letkf_core.f90:70-81, 90-158): U has nx+1 columns and V ny+1 rows of
+# which only the mass-grid ones are analysed (Q2, :209-210; mass-point altitude, :192-193);
+# W and PH have nz+1 levels; MU one; QVAPOR and the hydrometeors get letkf_tune_q (:252-278).
+CYCLE = (("U", 1.6, "u"), ("V", 1.6, "v"), ("W", 1.6, "w"), ("T", 1.6, "m"),
+         ("QVAPOR", 1.6, "q"), ("QRAIN", 1.1, "q"), ("QSNOW", 1.1, "q"), ("QGRAUP", 1.1, "q"),
+         ("QHAIL", 1.1, "q"), ("QNRAIN", 1.1, "q"), ("QNSNOW", 1.1, "q"),
+         ("QNGRAUPEL", 1.1, "q"), ("QNHAIL", 1.1, "q"), ("MU", 1.1, "mu"), ("P", 1.1, "m"),
+         ("PH", 1.1, "w"))
+
+
+def time_cycle(core, w, world, dev, x, y, alt):
+    """Wall-clock of one analysis cycle on this rank's rows: every var_update entry of
+    input.nml analysed with the configuration's obs set and localisation (one obs type, so
+    the k-d trees are built once and shared, as the tree cache does for variables of equal
+    localisation).  Slabs are made on the device before the timed region (synthetic
+    N(0,1) members: the cost does not depend on the values); max over ranks."""
+    cfg, k, nz = w.extra["cfg"], w.k, w.nz
+    ny, nx = x.shape
+    top = alt[-1:] + 400.0                      # one staggered level above the top
+    runs = []
+    for name, infl, kind in CYCLE:
+        xs, ys, al, nzv, nxv, nyv = x, y, alt, nz, nx, ny
+        if kind == "u":
+            nxv = nx + 1
+            xs = torch.cat([x, x[:, -1:] + 2e3], 1).contiguous()
+            ys = torch.cat([y, y[:, -1:]], 1).contiguous()
+        elif kind == "v":
+            nyv = ny + 1
+            xs = torch.cat([x, x[-1:]], 0).contiguous()
+            ys = torch.cat([y, y[-1:] + 2e3], 0).contiguous()
+        elif kind == "w":
+            nzv = nz + 1
+            al = torch.cat([alt, top], 0).contiguous()
+        elif kind == "mu":
+            nzv = 1
+            al = alt[:1].contiguous()
+        var = torch.randn((k, nzv, nyv, nxv), device=dev)
+        vp = synth.radar_var_params(cfg["hclr"], cfg["vclr"], cfg["max_lz"], cfg["err"],
+                                    cfg["err_rej"], cfg["radar_type"], multi_infl=infl)
+        vp.tune_q = 1 if kind == "q" else 0
+        runs.append((name, vp, abi.make_slab(xs, ys, al, var, memory=abi.MEM_DEVICE,
+                                             ix_lim=nx, iy_lim=ny), var))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    per = {}
+    t0 = time.perf_counter()
+    for name, vp, slab, _ in runs:
+        ta = time.perf_counter()
+        core.analyze_var(vp, slab)
+        per[name] = round((time.perf_counter() - ta) * 1e3, 2)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    if world > 1:
+        t = torch.tensor([ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+    return {"cycle_ms": ms, "variables": len(CYCLE), "per_variable_ms_rank0": per,
+            "note": "input.nml var_update on this configuration's grid and obs set; "
+                    "U/V staggered (Q2), W/PH nz+1 levels, MU 1 level, tune_q on the Q "
+                    "species; analysis only (no member<->column transposes, no file I/O)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,6 +174,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--transposes", action="store_true",
                     help="also time one member<->column transpose of the variable (detail only)")
+    ap.add_argument("--no-cycle", action="store_true",
+                    help="skip the wall-clock-per-cycle detail (16 var_update entries)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -122,27 +188,26 @@ def main():
 
     w = synth.make(args.config, rows=(rank, world) if world > 1 else None)
     k = w.k
-    # ---- observation set: generated on rank 0, one RCCL broadcast --------------------------
+    # ---- observation set: packed on rank 0 (obs-set wire format), broadcast over RCCL --------
     n = w.obs.shape[0]
-    pack = torch.empty(cdist.packed_len(n, k), dtype=torch.float32, device=dev)
-    if rank == 0:
-        pack.copy_(torch.from_numpy(cdist.pack_radar(w.obs_xyz, w.obs, w.hdxb)))
+    types = [dict(family=1, type_id=w.radar_type, xyz=w.obs_xyz, obs=w.obs, hdxb=w.hdxb)]
     bcast_ms = 0.0
     if world > 1:
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        cdist.broadcast_obs(pack, src=0)
+        _, types = cdist.broadcast_obs_set(types if rank == 0 else None, k, dev, src=0)
         torch.cuda.synchronize()
         bcast_ms = (time.perf_counter() - t0) * 1e3
-    oxyz, oobs, ohdxb = cdist.unpack_radar(pack, n, k)
+    else:
+        _, types = cdist.unpack_obs_set(torch.from_numpy(cdist.pack_obs_set(types, k)).to(dev))
     # ---- slab in HBM ---------------------------------------------------------------------------
     x, y, alt = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt))
     var = torch.from_numpy(w.var).to(dev)
     torch.cuda.synchronize()
 
     core = abi.Core(k, device=local)
-    core.set_obs(abi.ObsSetBuilder(abi.MEM_DEVICE).add_radar(w.radar_type, oxyz, oobs, ohdxb).build())
+    core.set_obs(cdist.builder_from(types, abi.MEM_DEVICE).build())
     slab = abi.make_slab(x, y, alt, var, memory=abi.MEM_DEVICE)
 
     for _ in range(args.warmup):
@@ -170,6 +235,7 @@ def main():
         pts_total = float(pts_local)
 
     tr_detail = time_transposes(core, w, k, rank, world, dev) if args.transposes else None
+    cycle = None if args.no_cycle else time_cycle(core, w, world, dev, x, y, alt)
 
     if rank == 0:
         jacobi = os.environ.get("CWBL_SOLVER") == "jacobi"
@@ -239,6 +305,7 @@ def main():
                 "nonconverged": sum(s.nonconverged for s in stats),
                 "obs_bcast_ms": bcast_ms,
                 "transposes": tr_detail,
+                "cycle": cycle,
             },
             "cpu_baseline": None,
         }

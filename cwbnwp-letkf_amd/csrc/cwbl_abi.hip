@@ -508,6 +508,11 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   long long B = (long long)(S.ws_bytes / per_pt);
   B = std::max<long long>(std::min<long long>(B, npts), 256);
   B = std::min<long long>(B, 1 << 22);
+  {  // equal batches (a short last batch is all tail), whole list groups
+    const long long nbat = (npts + B - 1) / B;
+    B = (npts + nbat - 1) / nbat;
+    B = (B + kListLanes - 1) / kListLanes * kListLanes;
+  }
   HIPCHK(S.nbr_cnt.ensure((size_t)B * nt * 4));
   HIPCHK(S.nbr_idx.ensure((size_t)((B + kListLanes - 1) / kListLanes) * kListLanes *
                           std::max(list_cap, 1) * 4));

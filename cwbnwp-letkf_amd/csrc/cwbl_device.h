@@ -345,10 +345,11 @@ __device__ __forceinline__ int stage_columns(
     const int ncol = (int)(c1 - c0);
     for (int base = 0; base < ncol; base += CHUNK) {
       const int nsl = min(CHUNK, ncol - base);
-      if (lane < nsl) ch.yo[lane] = (E)yo_in[c0 + base + lane];
-      for (int e = lane; e < nsl * KP; e += NT) {
+      // the whole chunk is written (zeros past nsl), as on the analysis path
+      if (lane < CHUNK) ch.yo[lane] = lane < nsl ? (E)yo_in[c0 + base + lane] : (E)0.0f;
+      for (int e = lane; e < CHUNK * KP; e += NT) {
         const int s = e / KP, m = e - s * KP;
-        ch.yb[s][m] = m < k ? (E)yb_in[(c0 + base + s) * k + m] : (E)0.0f;
+        ch.yb[s][m] = (s < nsl && m < k) ? (E)yb_in[(c0 + base + s) * k + m] : (E)0.0f;
       }
       __syncthreads();
       accumulate(nsl);
@@ -436,20 +437,32 @@ __device__ __forceinline__ void assemble_point_mfma(
   const int kk = lane >> 4, m = lane & 15;
   ptot = stage_columns<KP, CHUNK, ASSEMBLED>(
       ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in, [&](int nsl) {
-        for (int s0 = 0; s0 < (c.debug_stop == 11 ? 0 : nsl); s0 += 4) {
-          const int s = s0 + kk;
-          const bool live = s < nsl;
+        // Column s = s0 + kk of the chunk feeds k-slot kk; every staged column past nsl is
+        // zero (stage_columns writes the whole chunk), so the operand reads need no
+        // predicate: row 16 I + m of tile row I is yb (row < KP), yo (row == KP) or 0.
+        // Branch-free reads, and the next 4 columns' reads are issued before this group's
+        // MFMAs, so the LDS latency hides behind the matrix pipe.
+        static_assert(CHUNK % 4 == 0, "k-slots");
+        float f[L::NT], fy;
+        auto load = [&](int s) {
+#pragma unroll
+          for (int I = 0; I < L::NT; ++I) {
+            const int row = 16 * I + m;
+            f[I] = ch.yb[s][row < KP ? row : KP - 1];
+          }
+          fy = ch.yo[s];
+        };
+        const int nl = c.debug_stop == 11 ? 0 : nsl;
+        if (nl > 0) load(kk);
+        for (int s0 = 0; s0 < nl; s0 += 4) {
           double op[L::NT];
 #pragma unroll
           for (int I = 0; I < L::NT; ++I) {
             const int row = 16 * I + m;
-            float f = 0.0f;
-            if (live) {
-              if (row < KP) f = ch.yb[s][row];
-              else if (L::YO_ROW && row == KP) f = ch.yo[s];
-            }
-            op[I] = (double)f;
+            const float v = row < KP ? f[I] : ((L::YO_ROW && row == KP) ? fy : 0.0f);
+            op[I] = (double)v;
           }
+          if (s0 + 4 < nl) load(s0 + 4 + kk);
           int t = 0;
 #pragma unroll
           for (int I = 0; I < L::NT; ++I)

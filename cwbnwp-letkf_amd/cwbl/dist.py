@@ -3,7 +3,7 @@
 The analysis shards embarrassingly: grid columns are dealt to ranks and points never
 communicate.  The only exchange is ONE broadcast of the packed observation set from the
 rank that read it (RCCL over xGMI on MI355X, backend "nccl"; gloo on CPU for tests).  It
-replaces the reference's ibcast/iallgatherv chain (module_gts_omboma.f90:532-605,
+replaces the reference's ibcast/iallgatherv chain (module_gts_omboma.f90:524-611,
 module_radar.f90:143-180).  Row dealing is cyclic with block 1, as the reference's
 decomposition (module_mpi_util.f90:73-188), which balances the uneven obs density.
 """
@@ -15,6 +15,123 @@ def shard_rows(ny, rank, world):
     return np.arange(rank, ny, world)
 
 
+# ---- wire format of a whole observation set ------------------------
+# One float32 buffer; integers travel as int32 bit patterns:
+#   [0] WIRE_MAGIC  [1] ntypes  [2] k
+#   [3 + 4t .. 6 + 4t]  family (0 GTS, 1 radar), type_id, nvar, nobs of type t
+#   then, type by type in header order, the cwbl_obs_set arrays in the reference's layouts
+#   (module_gts_omboma.f90:18-21, module_radar.f90:13-16):
+#     GTS:   xyz (n,3) | obs (n,nvar) | error (n,nvar) | hdxb (k,n,nvar) | qc (k,n,nvar) int32
+#     radar: xyz (n,3) | obs (n,) | hdxb (k,n)
+# The reference sends these as ~8 ibcasts and 2 iallgatherv per GTS type and 5 ibcasts + 1
+# iallgatherv per radar type, after an mpi_bcast of the counts; here the counts ride in the
+# header and the whole set is one message (preceded by its length).
+WIRE_MAGIC = 0x4C4B4631  # "LKF1"
+
+
+def _type_words(family, nvar, n, k):
+    return 3 * n + (2 * n * nvar + 2 * k * n * nvar if family == 0 else n + k * n)
+
+
+def pack_obs_set(types, k):
+    """types: dicts {family, type_id, xyz, obs, hdxb} (+ error, qc for GTS), numpy arrays in
+    the layouts above (ObsSetBuilder's).  Returns the float32 wire buffer."""
+    hdr = [WIRE_MAGIC, len(types), int(k)]
+    parts = []
+    for t in types:
+        fam = int(t["family"])
+        xyz = np.ascontiguousarray(t["xyz"], np.float32)
+        n = int(xyz.shape[0])
+        obs = np.ascontiguousarray(t["obs"], np.float32)
+        nvar = int(obs.shape[1]) if fam == 0 else 1
+        hdr += [fam, int(t["type_id"]), nvar, n]
+        parts.append(xyz.ravel())
+        if fam == 0:
+            parts += [obs.ravel(), np.ascontiguousarray(t["error"], np.float32).ravel(),
+                      np.ascontiguousarray(t["hdxb"], np.float32).ravel(),
+                      np.ascontiguousarray(t["qc"], np.int32).view(np.float32).ravel()]
+        else:
+            parts += [obs.ravel(), np.ascontiguousarray(t["hdxb"], np.float32).ravel()]
+    return np.concatenate([np.asarray(hdr, np.int32).view(np.float32)] + parts)
+
+
+def unpack_obs_set(buf):
+    """(k, types): per-type views into a wire buffer (numpy array or torch tensor, on any
+    device); qc views are int32."""
+    is_np = isinstance(buf, np.ndarray)
+
+    def ints(a):
+        if is_np:
+            return a.view(np.int32)
+        import torch
+        return a.view(torch.int32)
+
+    def host_ints(a):
+        v = ints(a)
+        return [int(x) for x in (v if is_np else v.cpu().numpy())]
+
+    magic, ntypes, k = host_ints(buf[:3])
+    if magic != WIRE_MAGIC:
+        raise ValueError(f"not an obs-set wire buffer (magic {magic:#x})")
+    hdr = host_ints(buf[3:3 + 4 * ntypes])
+    off = 3 + 4 * ntypes
+    types = []
+    for t in range(ntypes):
+        fam, tid, nvar, n = hdr[4 * t:4 * t + 4]
+
+        def take(cnt, shape):
+            nonlocal off
+            a = buf[off:off + cnt].reshape(shape)
+            off += cnt
+            return a
+
+        d = dict(family=fam, type_id=tid, nvar=nvar, nobs=n, xyz=take(3 * n, (n, 3)))
+        if fam == 0:
+            d["obs"] = take(n * nvar, (n, nvar))
+            d["error"] = take(n * nvar, (n, nvar))
+            d["hdxb"] = take(k * n * nvar, (k, n, nvar))
+            d["qc"] = ints(take(k * n * nvar, (k, n, nvar)))
+        else:
+            d["obs"] = take(n, (n,))
+            d["hdxb"] = take(k * n, (k, n))
+        types.append(d)
+    if off != buf.shape[0]:
+        raise ValueError(f"wire buffer has {buf.shape[0]} words, header describes {off}")
+    return k, types
+
+
+def builder_from(types, memory):
+    """An abi.ObsSetBuilder holding the (unpacked) types."""
+    from . import abi
+    b = abi.ObsSetBuilder(memory)
+    for t in types:
+        if t["family"] == 0:
+            b.add_gts(t["type_id"], t["xyz"], t["obs"], t["error"], t["hdxb"], t["qc"])
+        else:
+            b.add_radar(t["type_id"], t["xyz"], t["obs"], t["hdxb"])
+    return b
+
+
+def broadcast_obs_set(types, k, device, src=0, group=None):
+    """The obs-set exchange of a cycle: `src` packs its set (`types`, ignored elsewhere),
+    every rank receives it into one buffer on `device`.  Two broadcasts: the 8-byte length,
+    then the set.  Returns (k, types) as views into the received buffer."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    if rank == src:
+        buf = torch.from_numpy(pack_obs_set(types, k)).to(device)
+        ln = torch.tensor([buf.shape[0]], dtype=torch.int64, device=device)
+    else:
+        ln = torch.zeros(1, dtype=torch.int64, device=device)
+    dist.broadcast(ln, src=src, group=group)
+    if rank != src:
+        buf = torch.empty(int(ln.item()), dtype=torch.float32, device=device)
+    dist.broadcast(buf, src=src, group=group)
+    return unpack_obs_set(buf)
+
+
+# ---- single radar type (the bench's synthetic set) ---------------------------------------
 def pack_radar(obs_xyz, obs, hdxb):
     """One float32 buffer: xyz (n,3) | obs (n,) | hdxb (k,n)."""
     return np.concatenate([np.asarray(obs_xyz, np.float32).ravel(),
@@ -33,7 +150,7 @@ def unpack_radar(buf, n, k):
 
 
 def broadcast_obs(buf, src=0, group=None):
-    """The single obs-set broadcast (torch tensor, any backend)."""
+    """Broadcast of a pre-sized packed buffer (torch tensor, any backend)."""
     import torch.distributed as dist
     dist.broadcast(buf, src=src, group=group)
     return buf
