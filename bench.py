@@ -184,7 +184,12 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL over xGMI; CWBL_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU
+        backend = os.environ.get("CWBL_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     w = synth.make(args.config, rows=(rank, world) if world > 1 else None)
     k = w.k

@@ -284,27 +284,41 @@ __device__ __forceinline__ int stage_columns(
       static_assert(KP % (2 * LPC) == 0, "bg row split");
       const int sl = lane % CHUNK, half = lane / CHUNK;
       const int *__restrict__ lst = nbr_idx + lbase;
+      // q / nvar for the (obs, variable) pair index q < 2^22: a float estimate and one
+      // correction each way (nvar is wave-uniform; 1 for radar)
+      const float rnv = 1.0f / (float)nvar;
+      auto divn = [&](int q) {
+        int j = (int)((float)q * rnv);
+        j -= j * nvar > q ? 1 : 0;
+        j += (j + 1) * nvar <= q ? 1 : 0;
+        return j;
+      };
       int slot_next = 0;
-      if (sl < min(CHUNK, npairs)) slot_next = gld(lst, list_slot(sl / nvar));
+      if (sl < min(CHUNK, npairs)) slot_next = gld(lst, list_slot(divn(sl)));
       for (int base = 0; base < npairs; base += CHUNK) {
         const int nsl = min(CHUNK, npairs - base);
         const bool live = sl < nsl;
         const int q = base + sl;
-        const int jn = q / nvar, v = q - jn * nvar;
+        const int jn = divn(q), v = q - jn * nvar;
         const int slot = slot_next;
         const int col = slot * nvar + v;
-        uint8_t okb = 0;
-        float err = 1.0f, omm = 0.0f;
-        f32x4 rd = {0.0f, 0.0f, 0.0f, 0.0f};
+        // the next chunk's slot first: it depends on nothing gathered below
+        const int nb = base + CHUNK;
+        if (sl < min(CHUNK, npairs - nb)) slot_next = gld(lst, list_slot(divn(nb + sl)));
+        // Gathers without a branch: a lane past nsl keeps the slot of an earlier chunk (or
+        // 0), a valid table index, and its column is zeroed by w = 0 below.  The bg row part
+        // goes first and as 16-B loads (b0 is a multiple of 4 floats: KP % 8 == 0), then
+        // the scalars; all addresses are formed before the first load.
         float2 g[VH];
+        const unsigned b0 = (unsigned)(col * KP + 2 * VH * half);
+        if constexpr (VH % 2 == 0) {
 #pragma unroll
-        for (int i = 0; i < VH; ++i) g[i] = make_float2(0.0f, 0.0f);
-        if (live) {
-          okb = gld(T.col_ok, (unsigned)col);
-          err = gld(T.col_err, (unsigned)col);
-          omm = gld(T.col_omm, (unsigned)col);
-          rd = gld4(reinterpret_cast<const float *>(T.rdata), 4u * (unsigned)slot);
-          const unsigned b0 = (unsigned)(col * KP + 2 * VH * half);
+          for (int i = 0; i < VH / 2; ++i) {
+            const f32x4 t = gld4(T.col_bg, b0 + 4u * i);
+            g[2 * i] = make_float2(t.x, t.y);
+            g[2 * i + 1] = make_float2(t.z, t.w);
+          }
+        } else {
           typedef float f32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
           for (int i = 0; i < VH; ++i) {
@@ -313,22 +327,25 @@ __device__ __forceinline__ int stage_columns(
             g[i] = make_float2(t.x, t.y);
           }
         }
-        // prefetch the next chunk's slots behind this chunk's gathers
-        const int nb = base + CHUNK;
-        if (sl < min(CHUNK, npairs - nb))
-          slot_next = gld(lst, list_slot((nb + sl) / nvar));
+        const uint8_t okb = gld(T.col_ok, (unsigned)col);
+        const float err = gld(T.col_err, (unsigned)col);
+        const float omm = gld(T.col_omm, (unsigned)col);
+        const f32x4 rd = gld4(reinterpret_cast<const float *>(T.rdata), 4u * (unsigned)slot);
         const bool ok = live && okb != 0;
-        float w = 0.0f, yo = 0.0f;
-        if (ok) {
-          w = error_inv(c.weight_function, err, slot_r2(rd, T.tree_dim, q0, q1, q2), ch.expt);
-          yo = omm * w;  // omm * error_inv (:451)
-        }
+        // computed for every lane and selected (a branch here would sink the rd/err/omm
+        // loads behind the ok-flag load: two round trips per chunk instead of one)
+        const float wv =
+            error_inv(c.weight_function, err, slot_r2(rd, T.tree_dim, q0, q1, q2), ch.expt);
+        const float w = ok ? wv : 0.0f;
+        const float yo = ok ? omm * wv : 0.0f;  // omm * error_inv (:451)
         ptot += __popcll(__ballot(ok && half == 0));  // counted by wave 0
         if (half == 0) ch.yo[sl] = (E)yo;
         E *dst = &ch.yb[sl][2 * VH * half];
 #pragma unroll
         for (int i = 0; i < VH; ++i) {
-          const float y0 = g[i].x * w, y1 = g[i].y * w;  // bg * error_inv (:452)
+          // bg * error_inv (:452); a rejected column (or a lane past nsl) stages exact
+          // zeros, whatever its gathered bg holds
+          const float y0 = ok ? g[i].x * w : 0.0f, y1 = ok ? g[i].y * w : 0.0f;
           if constexpr (sizeof(E) == 8) {
             *reinterpret_cast<double2 *>(dst + 2 * i) = make_double2((double)y0, (double)y1);
           } else {
