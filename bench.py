@@ -180,7 +180,8 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    # (modulo the visible GPUs: one GPU can host a multi-rank rehearsal)
+    local = int(os.environ.get("LOCAL_RANK", 0)) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -284,7 +285,10 @@ def main():
                 "k": k,
                 "n_obs": n,
                 "mean_p": nobs_sum / max(solved, 1),
-                "parallelism": f"column-sharded x{world}" + (", RCCL obs broadcast" if world > 1 else ""),
+                "parallelism": f"column-sharded x{world}" + (
+                    ", obs-set broadcast over " + ("RCCL" if dist.get_backend() == "nccl"
+                                                  else dist.get_backend())
+                    if world > 1 else ""),
             },
             "roofline": {
                 "bound": "mfma",
