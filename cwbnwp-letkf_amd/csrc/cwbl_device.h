@@ -343,9 +343,9 @@ __device__ __forceinline__ int stage_columns(
         E *dst = &ch.yb[sl][2 * VH * half];
 #pragma unroll
         for (int i = 0; i < VH; ++i) {
-          // bg * error_inv (:452); a rejected column (or a lane past nsl) stages exact
-          // zeros, whatever its gathered bg holds
-          const float y0 = ok ? g[i].x * w : 0.0f, y1 = ok ? g[i].y * w : 0.0f;
+          // bg * error_inv (:452); w = 0 zeroes a rejected column and a lane past nsl (its
+          // bg is a finite table entry of an earlier slot)
+          const float y0 = g[i].x * w, y1 = g[i].y * w;
           if constexpr (sizeof(E) == 8) {
             *reinterpret_cast<double2 *>(dst + 2 * i) = make_double2((double)y0, (double)y1);
           } else {
