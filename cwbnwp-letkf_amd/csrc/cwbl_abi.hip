@@ -98,6 +98,8 @@ struct State {
   bool have_obs = false;
   std::vector<std::unique_ptr<TreeBufs>> tree_cache;  // trees of the current obs set
   DevBuf tdesc, nbr_cnt, nbr_idx, info, stats;
+  DevBuf nbr_cnt2, nbr_idx2;                          // second list buffer (search overlap)
+  hipStream_t sstream = nullptr;                      // neighbour searches of later batches
   DevBuf sx, sy, salt, svar;                          // slab staging (host-memory calls)
   DevBuf bcol, byo, byb, bxb, bxa, bev;               // solve_batch staging
   DevBuf qxyz, qnf, qidx, qr2;                        // search staging
@@ -285,7 +287,7 @@ void release_obs() {
 
 void release_all() {
   release_obs();
-  for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.info, &S.stats, &S.sx,
+  for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.nbr_cnt2, &S.nbr_idx2, &S.info, &S.stats, &S.sx,
                     &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev,
                     &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad, &S.wsa})
     b->release();
@@ -293,6 +295,8 @@ void release_all() {
   S.events.clear();
   if (S.stream) (void)hipStreamDestroy(S.stream);
   S.stream = nullptr;
+  if (S.sstream) (void)hipStreamDestroy(S.sstream);
+  S.sstream = nullptr;
   S.inited = false;
 }
 
@@ -357,6 +361,7 @@ int cwbl_init(const cwbl_init_params *p) {
   S.q1_mode = p->q1_mode;
   S.ws_bytes = p->workspace_bytes ? p->workspace_bytes : (size_t(2) << 30);
   HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&S.sstream, hipStreamNonBlocking));
   {
     std::vector<double2> tab((size_t)kQuadLevels * 32);
     for (int l = 1; l <= kQuadLevels; ++l) quad_table(l, &tab[(size_t)(l - 1) * 32]);
@@ -513,9 +518,16 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     B = (npts + nbat - 1) / nbat;
     B = (B + kListLanes - 1) / kListLanes * kListLanes;
   }
-  HIPCHK(S.nbr_cnt.ensure((size_t)B * nt * 4));
-  HIPCHK(S.nbr_idx.ensure((size_t)((B + kListLanes - 1) / kListLanes) * kListLanes *
-                          std::max(list_cap, 1) * 4));
+  const long long nbat = (npts + B - 1) / B;
+  const size_t bytes_cnt = (size_t)B * nt * 4;
+  const size_t bytes_idx =
+      (size_t)((B + kListLanes - 1) / kListLanes) * kListLanes * std::max(list_cap, 1) * 4;
+  HIPCHK(S.nbr_cnt.ensure(bytes_cnt));
+  HIPCHK(S.nbr_idx.ensure(bytes_idx));
+  if (nbat > 1) {
+    HIPCHK(S.nbr_cnt2.ensure(bytes_cnt));
+    HIPCHK(S.nbr_idx2.ensure(bytes_idx));
+  }
   HIPCHK(S.info.ensure((size_t)B * sizeof(int2)));
   HIPCHK(S.stats.ensure(sizeof(DevStats)));
   HIPCHK(hipMemsetAsync(S.stats.p, 0, sizeof(DevStats), S.stream));
@@ -525,23 +537,39 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   c.list_cap = list_cap;
   const TreeDesc *dtrees = S.tdesc.as<TreeDesc>();
   DevStats *dst = S.stats.as<DevStats>();
-  int ev = 3;
+  // The searches run on S.sstream into two list buffers, the solves on S.stream: batch
+  // b + 1's search (latency-bound, integer/fp32) overlaps batch b's solve (FP64-bound).
+  // Search b waits for the inputs (e_ready) and for the solve of b - 2 (same buffer); solve b
+  // waits for search b.
+  hipEvent_t e_ready;  // inputs staged and the counters cleared
+  HIPCHK(event(3, &e_ready));
+  HIPCHK(hipEventRecord(e_ready, S.stream));
+  HIPCHK(hipStreamWaitEvent(S.sstream, e_ready, 0));
+  int ev = 4;
   std::vector<std::pair<int, int>> search_ev, solve_ev;
-  for (long long g0 = 0; g0 < npts; g0 += B) {
+  std::vector<int> done_ev;
+  for (long long bi = 0; bi < nbat; ++bi) {
+    const long long g0 = bi * B;
     const int nb = (int)std::min<long long>(B, npts - g0);
-    hipEvent_t a, b, cc;
-    HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b)); HIPCHK(event(ev + 2, &cc));
-    HIPCHK(hipEventRecord(a, S.stream));
-    HIPCHK(launch_search(S.stream, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb,
-                         S.nbr_cnt.as<int>(), S.nbr_idx.as<int>(), nullptr, dst));
-    HIPCHK(hipEventRecord(b, S.stream));
+    int *ncnt = (bi & 1) ? S.nbr_cnt2.as<int>() : S.nbr_cnt.as<int>();
+    int *nidx = (bi & 1) ? S.nbr_idx2.as<int>() : S.nbr_idx.as<int>();
+    hipEvent_t a, b, b2, cc, dn;
+    HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b)); HIPCHK(event(ev + 2, &b2));
+    HIPCHK(event(ev + 3, &cc)); HIPCHK(event(ev + 4, &dn));
+    if (bi >= 2) HIPCHK(hipStreamWaitEvent(S.sstream, S.events[done_ev[bi - 2]], 0));
+    HIPCHK(hipEventRecord(a, S.sstream));
+    HIPCHK(launch_search(S.sstream, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb, ncnt,
+                         nidx, nullptr, dst));
+    HIPCHK(hipEventRecord(b, S.sstream));
+    HIPCHK(hipStreamWaitEvent(S.stream, b, 0));
+    HIPCHK(hipEventRecord(b2, S.stream));
     if (S.kp > kMaxWaveKP)
-      HIPCHK(launch_solve_tq_big(S.stream, S.kp, false, dtrees, c, sd, g0, nb,
-                                 S.nbr_cnt.as<int>(), S.nbr_idx.as<int>(), nullptr, nullptr,
-                                 nullptr, nullptr, nullptr, S.info.as<int2>()));
+      HIPCHK(launch_solve_tq_big(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
+                                 nullptr, nullptr, nullptr, nullptr, nullptr,
+                                 S.info.as<int2>()));
     else if (S.jacobi)
-      HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, S.nbr_cnt.as<int>(),
-                                    S.nbr_idx.as<int>(), S.info.as<int2>()));
+      HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, ncnt, nidx,
+                                    S.info.as<int2>()));
     else if (S.tq4 && S.kp == kTq4KP) {
       // assembly -> workspace -> four-points-per-wave solve, in hand-off batches of Bs
       // points (a multiple of kListLanes, so a batch's neighbour lists start on a group)
@@ -556,21 +584,22 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
         const int ns = (int)std::min<long long>(Bs, nb - s0);
         HIPCHK(launch_assemble_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
-                                       S.nbr_cnt.as<int>() + s0 * nt,
-                                       S.nbr_idx.as<int>() + s0 * list_cap,
+                                       ncnt + s0 * nt, nidx + s0 * list_cap,
                                        S.info.as<int2>() + s0, S.wsa.as<double>()));
         HIPCHK(launch_solve_tq4(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
                                 S.info.as<int2>() + s0));
       }
     } else
-      HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, S.nbr_cnt.as<int>(),
-                             S.nbr_idx.as<int>(), nullptr, nullptr, nullptr, nullptr,
-                             nullptr, S.info.as<int2>()));
+      HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
+                             nullptr, nullptr, nullptr, nullptr, nullptr,
+                             S.info.as<int2>()));
     HIPCHK(hipEventRecord(cc, S.stream));
+    HIPCHK(hipEventRecord(dn, S.stream));  // this batch's lists are free again
     HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), nb, dst));
     search_ev.push_back({ev, ev + 1});
-    solve_ev.push_back({ev + 1, ev + 2});
-    ev += 3;
+    solve_ev.push_back({ev + 2, ev + 3});
+    done_ev.push_back(ev + 4);
+    ev += 5;
   }
   if (vp->tune_q) {  // letkf_driver's Q species post-step (:253-278), on the resident slab
     hipEvent_t a, b;
