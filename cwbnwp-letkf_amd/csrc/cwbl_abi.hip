@@ -730,6 +730,23 @@ int cwbl_vcoord_mean(const float *ph, long long n2d, int nz_ph, int k, int stagg
   return CWBL_OK;
 }
 
+int cwbl_member_sum(const float *fields, long long n, int nm, float *out) {
+  if (int rc = require_device()) return rc;
+  if (n < 0 || nm < 1 || (n > 0 && (!fields || !out)))
+    return fail(CWBL_ERR_ARG, "cwbl_member_sum: bad arguments");
+  HIPCHK(launch_member_sum(S.stream, fields, n, nm, out));
+  HIPCHK(hipStreamSynchronize(S.stream));
+  return CWBL_OK;
+}
+
+int cwbl_scale(float *x, long long n, float alpha) {
+  if (int rc = require_device()) return rc;
+  if (n < 0 || (n > 0 && !x)) return fail(CWBL_ERR_ARG, "cwbl_scale: bad arguments");
+  HIPCHK(launch_scale(S.stream, x, n, alpha));
+  HIPCHK(hipStreamSynchronize(S.stream));
+  return CWBL_OK;
+}
+
 int cwbl_search(int nobs, const float *obs_xyz, float hclr, float vclr, int max_lz_pts,
                 int nq, const float *q_xyz, int *nfound, int *idx, float *r2, int memory) {
   if (int rc = require_device()) return rc;

@@ -115,6 +115,9 @@ hipError_t launch_unpack_columns(hipStream_t s, const float *recv, const Decomp 
                                  float *global);
 hipError_t launch_vcoord_mean(hipStream_t s, const float *ph, long long n2d, int nz_ph, int k,
                               int stagger, float alpha, float *alt);
+hipError_t launch_member_sum(hipStream_t s, const float *fields, long long n, int nm,
+                             float *out);
+hipError_t launch_scale(hipStream_t s, float *x, long long n, float alpha);
 
 // letkf_tune_q over the analysed region of s.var (module_letkf_core.f90:702-733)
 hipError_t launch_tune_q(hipStream_t st, SlabDev s, int k);

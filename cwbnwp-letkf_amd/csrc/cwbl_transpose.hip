@@ -9,6 +9,8 @@
 //   pack_columns_kernel    letkf_scatter_grid send side (:224-258): global -> per-rank chunks
 //   unpack_columns_kernel  letkf_gather_grid receive side (:326-350): chunks -> global
 //   vcoord_mean_kernel     letkf_scatter_vcoord (:491-505): member mean of PH / g, destagger
+//   member_sum_kernel, scale_kernel   write_mean (module_grid.f90:744-840): the rank-local
+//                          member sum ahead of the one reduce, and the root's sscal
 // All three are HBM bound byte moves (no arithmetic worth a matrix core): one thread per
 // element of the global field, so the global side is read or written fully coalesced and
 // the chunk side is px interleaved contiguous streams per wavefront.
@@ -101,6 +103,25 @@ vcoord_mean_kernel(const float *__restrict__ ph, long long n2d, int nz_ph, int k
   }
 }
 
+// write_mean's member sum (module_grid.f90:744-822, the rank-local part): fp32, member order
+__global__ void __launch_bounds__(256)
+member_sum_kernel(const float *__restrict__ f, long long n, int nm, float *__restrict__ out) {
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n;
+       e += (long long)gridDim.x * 256) {
+    float s = 0.0f;
+    for (int m = 0; m < nm; ++m) s = s + f[e + (long long)m * n];
+    out[e] = s;
+  }
+}
+
+// sscal (module_grid.f90:827-...)
+__global__ void __launch_bounds__(256)
+scale_kernel(float *__restrict__ x, long long n, float alpha) {
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n;
+       e += (long long)gridDim.x * 256)
+    x[e] = alpha * x[e];
+}
+
 static dim3 grid_for(long long n) {
   const long long b = (n + 255) / 256;
   return dim3((unsigned)std::min<long long>(std::max<long long>(b, 1), 1 << 20));
@@ -128,6 +149,19 @@ hipError_t launch_vcoord_mean(hipStream_t s, const float *ph, long long n2d, int
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(vcoord_mean_kernel, grid_for(n), dim3(256), 0, s, ph, n2d, nz_ph, k,
                      stagger, alpha, alt);
+  return hipGetLastError();
+}
+
+hipError_t launch_member_sum(hipStream_t s, const float *fields, long long n, int nm,
+                             float *out) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(member_sum_kernel, grid_for(n), dim3(256), 0, s, fields, n, nm, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale(hipStream_t s, float *x, long long n, float alpha) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scale_kernel, grid_for(n), dim3(256), 0, s, x, n, alpha);
   return hipGetLastError();
 }
 

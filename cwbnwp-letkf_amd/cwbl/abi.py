@@ -86,6 +86,7 @@ class Stats(C.Structure):
 #: exported symbols of the product library (include/cwb_letkf_core.h)
 EXPORTS = ["cwbl_init", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch", "cwbl_search",
            "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
+           "cwbl_member_sum", "cwbl_scale",
            "cwbl_finalize", "cwbl_last_error", "cwbl_abi_version"]
 
 
@@ -226,12 +227,14 @@ def load_library(path=None):
     lib.cwbl_pack_columns.argtypes = [vp] + [C.c_int] * 5 + [vp]
     lib.cwbl_unpack_columns.argtypes = [vp] + [C.c_int] * 5 + [vp]
     lib.cwbl_vcoord_mean.argtypes = [vp, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_float, vp]
+    lib.cwbl_member_sum.argtypes = [vp, C.c_longlong, C.c_int, vp]
+    lib.cwbl_scale.argtypes = [vp, C.c_longlong, C.c_float]
     lib.cwbl_finalize.argtypes = []
     lib.cwbl_last_error.restype = cp
     lib.cwbl_abi_version.restype = C.c_int
     for fn in ("cwbl_init", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch",
                "cwbl_search", "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
-               "cwbl_finalize"):
+               "cwbl_member_sum", "cwbl_scale", "cwbl_finalize"):
         getattr(lib, fn).restype = C.c_int
     return lib
 
@@ -304,6 +307,14 @@ class Core:
     def vcoord_mean(self, ph, n2d, nz_ph, k, stagger, g, alt):
         """letkf_scatter_vcoord's member mean of PH/g + destagger (:491-505)."""
         self._check(self.lib.cwbl_vcoord_mean(_ptr(ph), n2d, nz_ph, k, stagger, g, _ptr(alt)))
+
+    def member_sum(self, fields, n, nm, out):
+        """write_mean's rank-local member sum (module_grid.f90:744-822): fields (nm, n)."""
+        self._check(self.lib.cwbl_member_sum(_ptr(fields), n, nm, _ptr(out)))
+
+    def scale(self, x, n, alpha):
+        """sscal (module_grid.f90:827-...)."""
+        self._check(self.lib.cwbl_scale(_ptr(x), n, alpha))
 
     def finalize(self):
         self._check(self.lib.cwbl_finalize())

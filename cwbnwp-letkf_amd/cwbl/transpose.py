@@ -139,6 +139,63 @@ class Transposer:
         if self.device.type == "cuda":
             self.torch.cuda.synchronize(self.device)
 
+    # ---- write_mean's ensemble mean (module_grid.f90:700-840) -------
+    def write_mean(self, fields, root=0):
+        """fields: {m: [device tensors]} — the same list of analysed fields (psfc, mu, u, ...,
+        any shapes) for every member this rank owns.  Returns, on `root`, the list of the
+        ensemble means (sum over members * nmember_inv), None elsewhere.
+
+        The reference reduces each field separately over the member ranks (one mpi_reduce
+        per field, :744-822, 14-20 of them) and scales on the root with sscal (:827-...).
+        Here the fields are packed into one buffer per member, the members a rank holds are
+        summed on the device in member order (cwbl_member_sum), ONE reduce (RCCL over xGMI
+        with backend nccl) combines the ranks, and the root scales (cwbl_scale).  The sum
+        order across ranks is the collective's, as it is MPI's in the reference, so the
+        means agree with the reference to fp32 rounding of the sums, not bit for bit."""
+        torch, dist = self.torch, self.dist
+        mine = self.owned()
+        shapes = [tuple(t.shape) for t in fields[mine[0]]] if mine else []
+        if self.world > 1:  # every rank needs the layout (a rank may own no member)
+            box = [shapes]
+            dist.broadcast_object_list(box, src=self._peer(self.owner(0)), group=self.group)
+            shapes = box[0]
+        sizes = [int(np.prod(sh)) for sh in shapes]
+        n = int(sum(sizes))
+        packed = torch.empty((max(len(mine), 1), n), dtype=torch.float32, device=self.device)
+        for i, m in enumerate(mine):
+            off = 0
+            for t, sz in zip(fields[m], sizes):
+                packed[i, off:off + sz].copy_(t.reshape(-1))
+                off += sz
+        total = torch.empty(n, dtype=torch.float32, device=self.device)
+        self._sync()
+        if mine:
+            self._member_sum(packed, n, len(mine), total)
+        else:
+            total.zero_()
+        if self.world > 1:
+            if self.backend == "nccl":
+                dist.reduce(total, dst=self._peer(root), op=dist.ReduceOp.SUM, group=self.group)
+            else:  # gloo (tests): host staging
+                h = total.cpu()
+                dist.reduce(h, dst=self._peer(root), op=dist.ReduceOp.SUM, group=self.group)
+                total.copy_(h)
+        if self.rank != root:
+            return None
+        self._sync()
+        self._scale(total, n, float(np.float32(1.0) / np.float32(self.k)))  # nmember_inv
+        out, off = [], 0
+        for sh, sz in zip(shapes, sizes):
+            out.append(total[off:off + sz].reshape(sh))
+            off += sz
+        return out
+
+    def _member_sum(self, packed, n, nm, out):
+        self.core.member_sum(packed, n, nm, out)
+
+    def _scale(self, x, n, alpha):
+        self.core.scale(x, n, alpha)
+
     # ---- letkf_scatter_grid (:190-262) ---------------------------------------------------------
     def scatter_grid(self, fields, nz, stagger=0, out=None):
         """fields: {m: (nz, ny', nx') device tensor} for the members this rank owns.

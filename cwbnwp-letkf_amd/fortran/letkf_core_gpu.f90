@@ -70,6 +70,7 @@ module letkf_core_gpu
 
     public :: cwbl_init, cwbl_set_obs, cwbl_analyze_var, cwbl_solve_batch, cwbl_search, &
               cwbl_pack_columns, cwbl_unpack_columns, cwbl_vcoord_mean, &
+              cwbl_member_sum, cwbl_scale, &
               cwbl_finalize, cwbl_abi_version, cwbl_error, cwbl_check
 
     interface
@@ -129,6 +130,22 @@ module letkf_core_gpu
             integer(c_int),       value :: nz_ph, k, stagger
             real(c_float),        value :: g
         end function cwbl_vcoord_mean
+
+        ! write_mean (module_grid.f90:744-840): member sum of device fields(n, nm), member
+        ! slowest, and sscal; the cross-rank sum between the two is one reduce (MPI or RCCL)
+        integer(c_int) function cwbl_member_sum(fields, n, nm, out) bind(C, name='cwbl_member_sum')
+            import :: c_int, c_long_long, c_ptr
+            type(c_ptr),          value :: fields, out
+            integer(c_long_long), value :: n
+            integer(c_int),       value :: nm
+        end function cwbl_member_sum
+
+        integer(c_int) function cwbl_scale(x, n, alpha) bind(C, name='cwbl_scale')
+            import :: c_int, c_long_long, c_float, c_ptr
+            type(c_ptr),          value :: x
+            integer(c_long_long), value :: n
+            real(c_float),        value :: alpha
+        end function cwbl_scale
 
         integer(c_int) function cwbl_finalize() bind(C, name='cwbl_finalize')
             import :: c_int

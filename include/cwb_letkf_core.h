@@ -229,6 +229,19 @@ int         cwbl_unpack_columns(const float *recv, int nx, int ny, int nz, int p
 int         cwbl_vcoord_mean(const float *ph, long long n2d, int nz_ph, int k, int stagger,
                              float g, float *alt);
 
+/* ---- ensemble mean of the analysis (write_mean, module_grid.f90:700-840; SURVEY.md §8(f)
+ * rank 4) ------------------------------------------------------------------------------------
+ * The reference sums every analysed field over the member ranks with one mpi_reduce each
+ * (:744-822) and scales the root's sums by nmember_inv with sscal (:827-...).  Here a rank
+ * sums the members it holds (cwbl/transpose.py deals k/N members per rank), all fields packed
+ * in one buffer; ONE RCCL reduce of that buffer follows, then the scale on the root.  Device
+ * pointers; each call has completed when it returns. */
+/* out(i) = sum over m = 0..nm-1 of fields(i, m), fp32, sequential in member order;
+ * fields(n, nm) member slowest. */
+int         cwbl_member_sum(const float *fields, long long n, int nm, float *out);
+/* x(i) = alpha * x(i) (sscal, :827-...). */
+int         cwbl_scale(float *x, long long n, float alpha);
+
 int         cwbl_finalize(void);
 const char *cwbl_last_error(void);
 int         cwbl_abi_version(void);

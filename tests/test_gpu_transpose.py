@@ -104,3 +104,44 @@ def test_transposer_two_processes_real_kernels(tmp_path):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), k, nx, ny, nz), nprocs=world,
              join=True)
     check_plan(str(tmp_path), world, k, nx, ny, nz)
+
+
+@pytest.mark.parametrize("nm,n", [(1, 1000), (5, 100_003), (40, 2_000_000)])
+def test_member_sum_and_scale_kernels(nm, n):
+    """cwbl_member_sum (fp32, member order) and cwbl_scale (sscal) bit for bit against the
+    same operations in numpy."""
+    c = core()
+    rng = np.random.default_rng(nm)
+    f = rng.normal(size=(nm, n)).astype(np.float32)
+    dev = torch.device("cuda:0")
+    fd = torch.from_numpy(f).to(dev)
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    c.member_sum(fd, n, nm, out)
+    acc = np.zeros(n, np.float32)
+    for m in range(nm):
+        acc = acc + f[m]
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), acc.view(np.uint32))
+    inv = np.float32(1.0) / np.float32(nm)
+    c.scale(out, n, float(inv))
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), (inv * acc).view(np.uint32))
+
+
+def test_write_mean_single_rank():
+    """write_mean through the Transposer with the real kernels, one rank holding all k
+    members: the member-order sum times nmember_inv, bit for bit."""
+    k = 8
+    c = core(k)
+    t = tr.Transposer(c, k, 10, 7, device=torch.device("cuda:0"))
+    rng = np.random.default_rng(2)
+    allf = {m: [rng.normal(size=(7, 10)).astype(np.float32),
+                rng.normal(size=(4, 7, 11)).astype(np.float32)] for m in range(k)}
+    fields = {m: [torch.from_numpy(a).cuda() for a in allf[m]] for m in range(k)}
+    out = t.write_mean(fields)
+    inv = np.float32(1.0) / np.float32(k)
+    for i in range(2):
+        acc = np.zeros_like(allf[0][i])
+        for m in range(k):
+            acc = acc + allf[m][i]
+        np.testing.assert_array_equal(out[i].cpu().numpy().view(np.uint32),
+                                      (inv * acc).view(np.uint32))

@@ -75,6 +75,15 @@ class OracleCore:
     def vcoord_mean(self, ph, n2d, nz_ph, k, stagger, gconst, alt):
         alt.copy_(torch.from_numpy(mo.vcoord_mean(ph.numpy(), stagger, np.float32(gconst))))
 
+    def member_sum(self, fields, n, nm, out):
+        acc = np.zeros(n, np.float32)
+        for m in range(nm):  # fp32, member order (cwbl_member_sum)
+            acc = acc + fields[m].numpy()
+        out.copy_(torch.from_numpy(acc))
+
+    def scale(self, x, n, alpha):
+        x.copy_(torch.from_numpy(np.float32(alpha) * x.numpy()))
+
 
 def _free_port():
     s = socket.socket()
@@ -171,3 +180,56 @@ def test_oracle_vcoord_mean_matches_mkl_sgemv(k, stagger):
     if mkl is None:
         pytest.skip("MKL not available")
     np.testing.assert_array_equal(mo.vcoord_mean(ph, stagger), mkl)
+
+
+def _mean_fields(k, seed=8):
+    """Per member the write_mean field list: 2-D (psfc-like), staggered U-like, 3-D."""
+    rng = np.random.default_rng(seed)
+    return {m: [rng.normal(size=(7, 10)).astype(np.float32),
+                rng.normal(size=(3, 7, 11)).astype(np.float32),
+                rng.normal(size=(3, 7, 10)).astype(np.float32) + 280.0] for m in range(k)}
+
+
+def _mean_worker(rank, world, port, out_dir, k):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = tr.Transposer(OracleCore(), k, 10, 7, device=torch.device("cpu"))
+    allf = _mean_fields(k)
+    mine = {m: [torch.from_numpy(a.copy()) for a in allf[m]] for m in t.owned()}
+    out = t.write_mean(mine, root=0)
+    if rank == 0:
+        np.savez(os.path.join(out_dir, "mean.npz"), *[o.numpy() for o in out])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k", [(2, 5), (3, 8)])
+def test_write_mean_gloo(tmp_path, world, k):
+    """write_mean's ensemble mean (module_grid.f90:700-840) through the Transposer: per-rank
+    member sums, one reduce, the root's sscal by nmember_inv.  At 2 ranks the cross-rank sum
+    is a single (commutative) add, so the result is bit-exact against the same order in
+    numpy; at 3 ranks gloo's reduction order is its own, so the check is fp32 rounding."""
+    mp.spawn(_mean_worker, args=(world, _free_port(), str(tmp_path), k), nprocs=world,
+             join=True)
+    got = np.load(tmp_path / "mean.npz")
+    allf = _mean_fields(k)
+    inv = np.float32(1.0) / np.float32(k)
+    for i in range(3):
+        parts = []
+        for r in range(world):
+            acc = np.zeros_like(allf[0][i])
+            for m in range(r, k, world):
+                acc = acc + allf[m][i]
+            parts.append(acc)
+        tot = parts[0]
+        for p in parts[1:]:
+            tot = tot + p
+        exp = inv * tot
+        g = got[f"arr_{i}"]
+        if world == 2:
+            np.testing.assert_array_equal(g.view(np.uint32), exp.view(np.uint32))
+        else:
+            np.testing.assert_allclose(g, exp, rtol=2e-6, atol=1e-6)
+        # and the reference's definition up to fp32 rounding
+        ref = np.mean(np.stack([allf[m][i] for m in range(k)]).astype(np.float64), axis=0)
+        np.testing.assert_allclose(g, ref, rtol=1e-5, atol=1e-5)
