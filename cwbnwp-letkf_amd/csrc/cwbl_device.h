@@ -264,6 +264,10 @@ __device__ __forceinline__ int stage_columns(
   int ptot = 0;
   if constexpr (!ASSEMBLED) {
     if (lane < 32) ch.expt[lane] = kExpT[lane];
+    // other waves read the table before the chunk loop's first barrier (error_inv below);
+    // LDS is not cleared between workgroups, so without this they can read a previous
+    // workgroup's bytes (one wave: the lanes' LDS ops are ordered, no barrier needed)
+    if constexpr (NT > 64) __syncthreads();
     for (int t = 0; t < c.ntrees; ++t) {
       const TreeDesc T = trees[t];  // by value: the fields live in SGPRs for the whole loop
       // get_lz normalisation of the point (module_localization.f90:243-253), as the search

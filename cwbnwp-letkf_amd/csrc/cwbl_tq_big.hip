@@ -21,6 +21,43 @@ namespace cwbl {
 constexpr int kBigThreads = 256;
 constexpr int kBigChunk = 32;
 
+// thread -> 4x4 blocks of the lower block triangle for the tridiagonalisation's benefit.
+// Blocks are numbered column-major over the triangle; block (bi, bj) is read and updated
+// while the step's block column J <= bj, so contiguous runs retire together.  A thread's
+// blocks come in 64-block slots, one per (wave, it):
+//   - the last `it` is partial (lanes < NBLK - 256 (NBL-1) - 64 wave, the same lanes as
+//     assemble_point's `tid + 256 it < NBLK`) and takes the first, shortest-lived blocks;
+//   - the full slots, in ascending lifetime s_0 .. s_{F-1}, are dealt snake-wise (it 0:
+//     wave w -> s_{F-1-w}, it 1: s_w, it 2: s_{F-5-w}), so every wave pairs a long-lived slot
+//     with a short-lived one and no wave carries the trailing matrix alone.
+// At k = 128 the heaviest wave runs 144 slot-steps of matvec + update instead of ~340 with
+// the row-major numbering (whose first slot holds rows that live to the last step).
+template <int KP>
+__device__ __forceinline__ void big_block_of_lane(int tid, int (&bi)[AsmLayout<KP, 256>::NBL],
+                                                  int (&bj)[AsmLayout<KP, 256>::NBL]) {
+  using L = AsmLayout<KP, 256>;
+  constexpr int NB = L::NB, NBL = L::NBL, F = 4 * (NBL - 1);
+  constexpr int R = L::NBLK - 256 * (NBL - 1);  // blocks in the partial slots
+  static_assert(NBL >= 1 && NBL <= 3 && R > 0, "slot plan");
+  const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+  for (int it = 0; it < NBL; ++it) {
+    int s;  // full-slot rank by lifetime
+    if (it == 0) s = F - 1 - wave;
+    else if (it == 1) s = wave;
+    else s = F - 5 - wave;
+    int b = it == NBL - 1 ? 64 * wave + lane : R + 64 * s + lane;
+    if (b >= L::NBLK) b = L::NBLK - 1;  // invalid lane of a partial slot (never used)
+    int cj = 0;
+    while (b >= NB - cj) {  // column cj holds blocks bi = cj .. NB-1
+      b -= NB - cj;
+      ++cj;
+    }
+    bj[it] = cj;
+    bi[it] = cj + b;
+  }
+}
+
 template <int KP>
 struct BigSmem {
   static constexpr int NB = KP / 4;
@@ -128,7 +165,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   }
 
   int bi[NBL], bj[NBL];
-  block_of_lane<KP, NT>(tid, bi, bj);
+  big_block_of_lane<KP>(tid, bi, bj);
   double acc[NBL][16];
   double b1acc;
   int ptot;
@@ -146,6 +183,13 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     return;
   }
 
+  if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the rest
+    double t = b1acc;
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) t += acc[it][0] + acc[it][15];
+    if (tid == 0 && info) info[gi] = make_int2(ptot, (int)t);
+    return;
+  }
   const double inflat_r8 = (double)c.inflat;
 #pragma unroll
   for (int it = 0; it < NBL; ++it) {
@@ -220,14 +264,16 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
       sm.tq[j + 1][1] = beta;
       sm.tau[j] = tau;
     }
-    if (tau == 0.0) continue;  // H_j = I (uniform)
+    // tau = 0 (H_j = I) runs the step too, as an exact no-op (w = 0): dead blocks (bj < J)
+    // are skipped below, and the row sums rely on every block's last live step
+    // (j = 4 bj + 3, where v vanishes on its columns) leaving exact zeros in its A v partials.
     const double v = tid == j + 1 ? 1.0 : x * scal;
     if (tid < KP) sm.vb[tid] = v;
     __syncthreads();
     double s1p = 0.0;
 #pragma unroll
     for (int it = 0; it < NBL; ++it) {
-      if (tid + NT * it < NBLK && bi[it] >= J) {
+      if (tid + NT * it < NBLK && bj[it] >= J) {
         double vi[4], vj[4];
         ld4(&sm.vb[4 * bi[it]], vi);
         ld4(&sm.vb[4 * bj[it]], vj);
@@ -278,7 +324,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < NBL; ++it) {
-      if (tid + NT * it < NBLK && bi[it] >= J) {
+      if (tid + NT * it < NBLK && bj[it] >= J) {
         double vi[4], vj[4], wi[4], wj[4];
         ld4(&sm.vb[4 * bi[it]], vi);
         ld4(&sm.vb[4 * bj[it]], vj);
@@ -307,6 +353,10 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   }
   __syncthreads();
 
+  if (c.debug_stop == 2) {
+    if (tid == 0 && info) info[gi] = make_int2(ptot, (int)(trace + ux + ub));
+    return;
+  }
   // ---- T^-1/2 u2 by quadrature (wave 0), u1^T T^-1 u2 exactly ----------------------------
   const double m = inflat_r8;
   const double ratio = trace / m - (double)(k - 1);
@@ -379,6 +429,10 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   double dsum = tid < KP ? sm.tq[tid][2] * zl : 0.0, z5 = 0.0, z6 = 0.0, z7 = 0.0;
   bsum4(dsum, z5, z6, z7);
   const double d = dsum;  // wbar . x' = u1 . T^-1 u2
+  if (c.debug_stop == 3) {
+    if (tid == 0 && info) info[gi] = make_int2(ptot, (int)d);
+    return;
+  }
 
   // ---- back-transform y <- Q y, two reflectors per reduction -----------------------------
   auto vrow = [&](const double *src, int j) {

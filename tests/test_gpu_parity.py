@@ -395,3 +395,26 @@ def test_driver_with_tune_q_vs_oracle():
     oracle().orc_tune_q(k, nx, ny, nz, case.ix_lim, case.iy_lim, xb.ctypes.data_as(C.c_void_p))
     rel = increment_rel_rms(var, ref, xb)
     assert rel <= INCR_TOL, rel
+
+
+@pytest.mark.parametrize("k", [65, 80, 96, 101, 127, 128])
+def test_large_k_random_batch_vs_oracle(k):
+    """The 256-thread kernel (KP = 96 / 128) on seeded random batches, every k class of
+    padding (k = KP, KP - 1, odd, just above 64): solve_batch vs the oracle's letkf_solve,
+    p from 1 (rank-one Yb Yb^T, zero reflectors) to 300."""
+    from helpers import oracle_solve
+    rng = np.random.default_rng(20261016 + k)
+    ps = [1, 2, 7, 40, 130, 300]
+    col = np.concatenate([[0], np.cumsum(ps)]).astype(np.int64)
+    yo = rng.normal(0, 1, col[-1]).astype(np.float32)
+    yb = rng.normal(0, 1, (col[-1], k)).astype(np.float32)
+    xb = rng.normal(5, 1, (len(ps), k)).astype(np.float32)
+    inflat = inflat_of(k, np.float32(1.1))
+    c = core(k)
+    xa, _ = c.solve_batch(col, yo, yb.reshape(-1), xb, inflat, 1, 0.7, 1, 0.3)
+    assert np.isfinite(xa).all()
+    for i, p in enumerate(ps):
+        ref, _ = oracle_solve(k, p, xb[i], yo[col[i]:col[i + 1]], yb[col[i]:col[i + 1]],
+                              inflat, 1, 0.7, 1, 0.3, want_evals=False)
+        rel = increment_rel_rms(xa[i], ref, xb[i])
+        assert rel <= INCR_TOL, (p, rel)
