@@ -73,6 +73,7 @@ struct BigSmem {
   double Ym[KP], Zm[KP];                  // quadrature sum / exact solve, walk order
   double tau[KP];
   double red[2][4][4];                    // [buffer][wave][value] of the block reductions
+  double red10[4][10];                    // [wave][value]: back-transform group reduction
   double pard;                            // sequential-sum partial handed wave to wave
   float parf;
   int ptot;
@@ -434,34 +435,86 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     return;
   }
 
-  // ---- back-transform y <- Q y, two reflectors per reduction -----------------------------
-  auto vrow = [&](const double *src, int j) {
-    return tid == j + 1 ? 1.0 : (tid > j + 1 && tid < k) ? src[tid] : 0.0;
-  };
-  int j = k - 3;
-  for (; j >= 1; j -= 2) {
-    __syncthreads();  // readers of col/col2 (previous pair) are done
-    CWBL_PUBLISH(j, sm.col);
-    CWBL_PUBLISH(j - 1, sm.col2);
-    __syncthreads();
-    const double t1 = sm.tau[j], t0 = sm.tau[j - 1];
-    const double v1 = t1 == 0.0 ? 0.0 : vrow(sm.col, j);
-    const double v0 = t0 == 0.0 ? 0.0 : vrow(sm.col2, j - 1);
-    double a1 = v1 * yl, b0 = v0 * yl, c01 = v0 * v1, z8 = 0.0;
-    bsum4(a1, b0, c01, z8);
-    yl = fma(-t1 * a1, v1, yl);
-    yl = fma(-t0 * fma(-t1 * a1, c01, b0), v0, yl);
+  // ---- back-transform y <- Q y = H_0 H_1 ... H_{k-3} y, four reflectors per reduction ------
+  // The reflectors of block column J live in the owners' registers (blocks (bi, J)), so a
+  // group of four is applied where it lies: the owners form v_q . y and v_q . v_p (q < p)
+  // from their rows (one 10-value reduction), every thread turns them into the coefficients
+  // of y -= sum_q c_q v_q (H_{4J+3} first), and the owners update their rows of y in LDS.
+  // Two barriers per four reflectors, and no reflector is published.
+  // First the register entries become exact reflector entries: 1 at row j+1, 0 at and above
+  // the diagonal (T is already in sm.tq).
+#pragma unroll
+  for (int it = 0; it < NBL; ++it) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 4 * bi[it] + r, col = 4 * bj[it] + q;
+        acc[it][4 * r + q] = row == col + 1 ? 1.0 : row > col + 1 ? acc[it][4 * r + q] : 0.0;
+      }
   }
-  if (j == 0) {
+  double *ys = sm.col;
+  if (tid < KP) ys[tid] = yl;
+  for (int JJ = (k - 3) >> 2; JJ >= 0 && k >= 3; --JJ) {
+    __syncthreads();  // y rows of the previous group are written
+    double dq[4] = {0.0, 0.0, 0.0, 0.0}, g[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) {
+      if (tid + NT * it < NBLK && bj[it] == JJ) {
+        double yr[4];
+        ld4(&ys[4 * bi[it]], yr);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double *V = &acc[it][4 * r];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dq[q] = fma(V[q], yr[r], dq[q]);
+          g[0] = fma(V[0], V[1], g[0]);
+          g[1] = fma(V[0], V[2], g[1]);
+          g[2] = fma(V[0], V[3], g[2]);
+          g[3] = fma(V[1], V[2], g[3]);
+          g[4] = fma(V[1], V[3], g[4]);
+          g[5] = fma(V[2], V[3], g[5]);
+        }
+      }
+    }
+    double z0 = 0.0, z1 = 0.0;
+    wave_sum4_dpp(dq[0], dq[1], dq[2], dq[3]);
+    wave_sum4_dpp(g[0], g[1], g[2], g[3]);
+    wave_sum4_dpp(g[4], g[5], z0, z1);
+    if (lane == 0) {
+      double *rw = sm.red10[wave];
+      rw[0] = dq[0]; rw[1] = dq[1]; rw[2] = dq[2]; rw[3] = dq[3];
+      rw[4] = g[0]; rw[5] = g[1]; rw[6] = g[2]; rw[7] = g[3]; rw[8] = g[4]; rw[9] = g[5];
+    }
     __syncthreads();
-    CWBL_PUBLISH(0, sm.col);
-    __syncthreads();
-    const double t0 = sm.tau[0];
-    const double v0 = t0 == 0.0 ? 0.0 : vrow(sm.col, 0);
-    double a0 = v0 * yl, z9 = 0.0, z10 = 0.0, z11 = 0.0;
-    bsum4(a0, z9, z10, z11);
-    yl = fma(-t0 * a0, v0, yl);
+    double t[10];
+#pragma unroll
+    for (int e = 0; e < 10; ++e)
+      t[e] = (sm.red10[0][e] + sm.red10[1][e]) + (sm.red10[2][e] + sm.red10[3][e]);
+    // t: d0..d3, G01 G02 G03 G12 G13 G23
+    const double tau0 = sm.tau[4 * JJ], tau1 = sm.tau[4 * JJ + 1];
+    const double tau2 = sm.tau[4 * JJ + 2], tau3 = sm.tau[4 * JJ + 3];
+    const double c3 = tau3 * t[3];
+    const double c2 = tau2 * fma(-c3, t[9], t[2]);
+    const double c1 = tau1 * fma(-c3, t[8], fma(-c2, t[7], t[1]));
+    const double c0 = tau0 * fma(-c3, t[6], fma(-c2, t[5], fma(-c1, t[4], t[0])));
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) {
+      if (tid + NT * it < NBLK && bj[it] == JJ) {
+        double yr[4];
+        ld4(&ys[4 * bi[it]], yr);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double *V = &acc[it][4 * r];
+          yr[r] = fma(-c0, V[0], fma(-c1, V[1], fma(-c2, V[2], fma(-c3, V[3], yr[r]))));
+        }
+        *reinterpret_cast<double2 *>(&ys[4 * bi[it]]) = make_double2(yr[0], yr[1]);
+        *reinterpret_cast<double2 *>(&ys[4 * bi[it] + 2]) = make_double2(yr[2], yr[3]);
+      }
+    }
   }
+  __syncthreads();
+  if (tid < KP) yl = ys[tid];
   const double sk = sqrt((double)(k - 1));
   float xal = tid < KP ? (float)(xb_mean + (d + sk * yl)) : 0.0f;
 
