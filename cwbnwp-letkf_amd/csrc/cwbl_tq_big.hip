@@ -170,9 +170,84 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   double acc[NBL][16];
   double b1acc;
   int ptot;
-  assemble_point<KP, kBigChunk, ASSEMBLED, NT>(sm.u.ch, trees, c, gi, tid, nbr_cnt, nbr_idx,
-                                               pt, col_off, yo_in, yb_in, bi, bj, acc, b1acc,
-                                               ptot);
+  if constexpr (KP == 128) {
+    // Matrix-core assembly (v_mfma_f64_16x16x4_f64): the 36 lower 16x16 tiles of Yb Yb^T,
+    // nine per wave: wave w owns tile rows w and 7-w (tiles (w, 0..w) and (7-w, 0..7-w)).
+    // The VALU form reads two float4 of the chunk from LDS per 16 FMAs and is LDS-bound;
+    // here a lane reads 11 floats per 4 columns for 9 MFMAs.  Then the tiles go through
+    // LDS, 16 at a time, into the 4x4 register blocks of the tridiagonalisation.
+    constexpr int NTW = 9;
+    static_assert(sizeof(sm.u.pb) >= 16 * 256 * sizeof(double), "tile staging area");
+    f64x4 tile[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) tile[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+    b1acc = 0.0;
+    const int m = lane & 15, kk = lane >> 4;
+    const int offA = 16 * wave + m, offB = 16 * (7 - wave) + m;
+    int offJ[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) offJ[t] = 16 * (t <= wave ? t : t - wave - 1) + m;
+    ptot = stage_columns<KP, kBigChunk, ASSEMBLED, NT>(
+        sm.u.ch, trees, c, gi, tid, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in,
+        [&](int nsl) {
+          // columns past nsl are staged as zeros (a multiple of 4 stays inside the chunk)
+          for (int s0 = 0; s0 < nsl; s0 += 4) {
+            const float *ys = sm.u.ch.yb[s0 + kk];
+            const double a = (double)ys[offA], b = (double)ys[offB];
+#pragma unroll
+            for (int t = 0; t < NTW; ++t)
+              tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(t <= wave ? a : b,
+                                                             (double)ys[offJ[t]], tile[t], 0, 0, 0);
+          }
+          if (tid < KP)  // Yb d (row KP of [Yb; yo] does not fit the tile padding)
+            for (int s = 0; s < nsl; ++s)
+              b1acc = fma((double)sm.u.ch.yb[s][tid], (double)sm.u.ch.yo[s], b1acc);
+        });
+    // block (bi, bj) lies in tile (I, J) = (bi/4, bj/4), held by wave min(I, 7-I) as its
+    // tile t = J (I <= 3) or 8 - I + J (I >= 4); staged in round t/4, slot 4 wave + t%4
+    int rnd[NBL], off[NBL];
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) {
+      const int I = bi[it] >> 2, J = bj[it] >> 2;
+      const int wI = I <= 3 ? I : 7 - I, t = I <= 3 ? J : 8 - I + J;
+      rnd[it] = t >> 2;
+      off[it] = (4 * wI + (t & 3)) * 256 + (4 * (bi[it] & 3)) * 16 + 4 * (bj[it] & 3);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[it][e] = 0.0;
+    }
+    double *tl = &sm.u.pb[0][0];
+#pragma unroll
+    for (int rd = 0; rd < 3; ++rd) {
+      __syncthreads();  // the chunk / the previous round's readers are done
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int t = 4 * rd + tt;
+        if (t < NTW) {
+          double *dst = tl + (4 * wave + tt) * 256;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dst[(kk + 4 * r) * 16 + m] = tile[t][r];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < NBL; ++it) {
+        if (tid + NT * it < NBLK && rnd[it] == rd) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double *src = tl + off[it] + 16 * r;
+            const double2 x0 = *reinterpret_cast<const double2 *>(src);
+            const double2 x1 = *reinterpret_cast<const double2 *>(src + 2);
+            acc[it][4 * r] = x0.x; acc[it][4 * r + 1] = x0.y;
+            acc[it][4 * r + 2] = x1.x; acc[it][4 * r + 3] = x1.y;
+          }
+        }
+      }
+    }
+  } else {
+    assemble_point<KP, kBigChunk, ASSEMBLED, NT>(sm.u.ch, trees, c, gi, tid, nbr_cnt, nbr_idx,
+                                                 pt, col_off, yo_in, yb_in, bi, bj, acc, b1acc,
+                                                 ptot);
+  }
   if (tid == 0) sm.ptot = ptot;  // counted by wave 0
   __syncthreads();
   ptot = sm.ptot;
