@@ -16,6 +16,8 @@
 //   - the reference's sequential fp32 member sums run wave after wave.
 #include "cwbl_device.h"
 
+#include <type_traits>
+
 namespace cwbl {
 
 constexpr int kBigThreads = 256;
@@ -292,22 +294,27 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     const double2 a1 = *reinterpret_cast<const double2 *>(p + 2);
     o[0] = a0.x; o[1] = a0.y; o[2] = a1.x; o[3] = a1.y;
   };
-  // column j of the lower block triangle -> dst (4 rows per block of block column j/4)
-#define CWBL_PUBLISH(jj, dst)                                                                \
-  do {                                                                                     \
-    const int J_ = (jj) >> 2, q_ = (jj) & 3;                                               \
-    _Pragma("unroll") for (int it = 0; it < NBL; ++it) {                                   \
-      if (tid + NT * it < NBLK && bj[it] == J_) {                                          \
-        double cv[4];                                                                      \
-        _Pragma("unroll") for (int r = 0; r < 4; ++r) {                                    \
-          const double a0 = acc[it][4 * r], a1 = acc[it][4 * r + 1];                       \
-          const double a2 = acc[it][4 * r + 2], a3 = acc[it][4 * r + 3];                   \
-          cv[r] = q_ == 0 ? a0 : q_ == 1 ? a1 : q_ == 2 ? a2 : a3;                         \
-        }                                                                                  \
-        *reinterpret_cast<double2 *>(&(dst)[4 * bi[it]]) = make_double2(cv[0], cv[1]);     \
-        *reinterpret_cast<double2 *>(&(dst)[4 * bi[it] + 2]) = make_double2(cv[2], cv[3]); \
-      }                                                                                    \
-    }                                                                                      \
+  // column j of the lower block triangle -> dst (4 rows per block of block column j/4); the
+  // column within the block is uniform, so a switch picks it (no per-value selects)
+  auto pub4 = [](double *d, double a0, double a1, double a2, double a3) {
+    *reinterpret_cast<double2 *>(d) = make_double2(a0, a1);
+    *reinterpret_cast<double2 *>(d + 2) = make_double2(a2, a3);
+  };
+#define CWBL_PUBLISH(jj, dst)                                                              \
+  do {                                                                                   \
+    const int J_ = (jj) >> 2, q_ = (jj) & 3;                                             \
+    _Pragma("unroll") for (int it = 0; it < NBL; ++it) {                                 \
+      if (tid + NT * it < NBLK && bj[it] == J_) {                                        \
+        double *d_ = &(dst)[4 * bi[it]];                                                 \
+        const double *a_ = acc[it];                                                      \
+        switch (q_) {                                                                    \
+          case 0: pub4(d_, a_[0], a_[4], a_[8], a_[12]); break;                          \
+          case 1: pub4(d_, a_[1], a_[5], a_[9], a_[13]); break;                          \
+          case 2: pub4(d_, a_[2], a_[6], a_[10], a_[14]); break;                         \
+          default: pub4(d_, a_[3], a_[7], a_[11], a_[15]); break;                        \
+        }                                                                                \
+      }                                                                                  \
+    }                                                                                    \
   } while (0)
 
   // ---- Householder tridiagonalisation ----------------------------------------------------
@@ -391,8 +398,19 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     double pp = 0.0;
     if (tid < KP && tid > j) {
       const double *prow = &sm.u.pb[tid >> 2][tid & 3];
+      // block columns < J hold exact zeros (dead blocks): start at the 8-column segment of J
+      auto rsum = [&](auto C) {
+        constexpr int c0 = decltype(C)::value;
+        double t = 0.0;
 #pragma unroll
-      for (int cb = 0; cb < SM::NB; ++cb) pp += prow[4 * cb];
+        for (int cb = c0; cb < SM::NB; ++cb) t += prow[4 * cb];
+        return t;
+      };
+      const int seg = J >> 3;
+      if (seg >= 3 && SM::NB > 24) pp = rsum(std::integral_constant<int, (SM::NB > 24 ? 24 : 0)>{});
+      else if (seg >= 2) pp = rsum(std::integral_constant<int, 16>{});
+      else if (seg >= 1) pp = rsum(std::integral_constant<int, 8>{});
+      else pp = rsum(std::integral_constant<int, 0>{});
     }
     const double p = (tid > j && tid < k) ? tau * pp : 0.0;
     const double w = fma(-0.5 * tau * s1, v, p);
@@ -412,12 +430,17 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
           for (int q = 0; q < 4; ++q)
             acc[it][4 * r + q] = fma(-vi[r], wj[q], fma(-wi[r], vj[q], acc[it][4 * r + q]));
         if (bj[it] == J) {  // keep v_j in the entries of column j the steps no longer read
+          const int r0 = j + 2 - 4 * bi[it];  // rows r >= r0 of the block
+          auto keep = [&](auto Q) {
+            constexpr int q = decltype(Q)::value;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const bool keep = 4 * bi[it] + r > j + 1;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              acc[it][4 * r + q] = (keep && q == qj) ? vi[r] : acc[it][4 * r + q];
+            for (int r = 0; r < 4; ++r) acc[it][4 * r + q] = r >= r0 ? vi[r] : acc[it][4 * r + q];
+          };
+          switch (qj) {
+            case 0: keep(std::integral_constant<int, 0>{}); break;
+            case 1: keep(std::integral_constant<int, 1>{}); break;
+            case 2: keep(std::integral_constant<int, 2>{}); break;
+            default: keep(std::integral_constant<int, 3>{}); break;
           }
         }
       }
