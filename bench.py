@@ -279,7 +279,7 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"{args.config}: {w.nx}x{w.extra['cfg']['ny']}x{w.nz} grid, k={k}, "
-                            f"{n} radar-VR-like obs (hclr {w.extra['cfg']['hclr']} km, vclr "
+                            f"{n} {'radar-dbz' if w.radar_type == abi.RADAR_DBZ else 'radar-VR'}-like obs (hclr {w.extra['cfg']['hclr']} km, vclr "
                             f"{w.extra['cfg']['vclr']} km), RTPP+RTPS, Gaussian localisation",
                 "grid_points": int(w.extra["cfg"]["nx"] * w.extra["cfg"]["ny"] * w.nz),
                 "k": k,
