@@ -248,6 +248,35 @@ def test_c2_full_size_properties():
     assert rel <= INCR_TOL, rel
 
 
+def test_c4_full_size_properties():
+    """Full C4 size (300x300x50, k=128, the 256-thread kernel): finite, bitwise reproducible
+    run to run (a cross-wave LDS race once showed up only as a few NaN points that moved
+    between runs), and the oracle on a column block."""
+    import ctypes as C
+    from cwbl import synth
+    w = synth.make("c4")
+    c = core(w.k)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    var = w.var.copy()
+    st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+    assert st.points == w.points
+    assert np.isfinite(var).all()
+    assert st.nonconverged == 0
+    var2 = w.var.copy()
+    c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var2))
+    np.testing.assert_array_equal(var.view(np.uint32), var2.view(np.uint32))
+    j0, i0, nb = 140, 150, 5
+    sub = lambda a: np.ascontiguousarray(a[..., j0:j0 + nb, i0:i0 + nb])  # noqa: E731
+    ref = sub(w.var).copy()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(sub(w.x), sub(w.y), sub(w.alt), ref)),
+                                  16, C.byref(abi.Stats()))
+    assert rc == 0
+    rel = increment_rel_rms(sub(var), ref, sub(w.var))
+    assert rel <= INCR_TOL, rel
+
+
 @pytest.mark.parametrize("name", ["driver_mixed.npz", "driver_gc_k40.npz"])
 def test_tq_and_jacobi_solvers_agree(name, monkeypatch):
     """The two solve kernels (eigendecomposition by Jacobi, CWBL_SOLVER=jacobi; and the
