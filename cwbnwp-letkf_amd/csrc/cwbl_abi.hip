@@ -100,6 +100,13 @@ struct State {
   DevBuf tdesc, nbr_cnt, nbr_idx, info, stats;
   DevBuf nbr_cnt2, nbr_idx2;                          // second list buffer (search overlap)
   hipStream_t sstream = nullptr;                      // neighbour searches of later batches
+  int lead_div = 0;                                   // first batch = npts / lead_div (0: off)
+  // Points per search/solve batch.  Measured on C2 (one GPU, ms per variable): 40 k 113,
+  // 70 k 110, 100 k 108, 150 k 107, 200 k 106, 500 k 109; and on an eighth of the grid (a
+  // rank of the 8-GPU run): 14.7-15.0 up to 150 k, 15.3 at 200 k, 16.6 at 285 k.  Smaller
+  // batches keep each batch's lists and hand-off records nearer the caches and overlap
+  // more of the search; below ~70 k the per-batch fixed costs win.
+  long long max_batch = 160000;
   DevBuf sx, sy, salt, svar;                          // slab staging (host-memory calls)
   DevBuf bcol, byo, byb, bxb, bxa, bev;               // solve_batch staging
   DevBuf qxyz, qnf, qidx, qr2;                        // search staging
@@ -373,6 +380,8 @@ int cwbl_init(const cwbl_init_params *p) {
   S.tq4 = true;
   if (const char *e = std::getenv("CWBL_TQ4")) S.tq4 = std::atoi(e) != 0;
   if (const char *e = std::getenv("CWBL_TQ4_SUB")) S.tq4_sub = std::atoll(e);
+  if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
+  if (const char *e = std::getenv("CWBL_MAX_BATCH")) S.max_batch = std::max(256LL, std::atoll(e));
   S.inited = true;
   return CWBL_OK;
 }
@@ -511,14 +520,27 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   // ---- batches of {search, solve} ---------------------------------------------------------
   const size_t per_pt = (size_t)list_cap * 4 + (size_t)nt * 4 + 8;
   long long B = (long long)(S.ws_bytes / per_pt);
+  B = std::min<long long>(B, S.max_batch);
   B = std::max<long long>(std::min<long long>(B, npts), 256);
   B = std::min<long long>(B, 1 << 22);
-  {  // equal batches (a short last batch is all tail), whole list groups
-    const long long nbat = (npts + B - 1) / B;
-    B = (npts + nbat - 1) / nbat;
-    B = (B + kListLanes - 1) / kListLanes * kListLanes;
+  // Batch plan: the first batch's search cannot overlap a solve, so it is short (a lead of
+  // 1/lead_div of the points); the rest are equal (a short last batch is all tail) and
+  // whole list groups.
+  std::vector<std::pair<long long, int>> plan;  // (g0, nb)
+  {
+    const auto round_up = [](long long v) { return (v + kListLanes - 1) / kListLanes * kListLanes; };
+    long long lead = S.lead_div > 0 ? round_up(npts / S.lead_div) : 0;
+    if (lead < 4 * kListLanes || lead >= npts) lead = 0;
+    if (lead > 0) plan.push_back({0, (int)std::min<long long>(lead, B)});
+    const long long g1 = plan.empty() ? 0 : plan[0].second, rest = npts - g1;
+    const long long nrest = (rest + B - 1) / B;
+    long long Br = round_up((rest + nrest - 1) / nrest);
+    for (long long g = g1; g < npts; g += Br)
+      plan.push_back({g, (int)std::min<long long>(Br, npts - g)});
+    B = 0;
+    for (const auto &b : plan) B = std::max<long long>(B, b.second);
   }
-  const long long nbat = (npts + B - 1) / B;
+  const long long nbat = (long long)plan.size();
   const size_t bytes_cnt = (size_t)B * nt * 4;
   const size_t bytes_idx =
       (size_t)((B + kListLanes - 1) / kListLanes) * kListLanes * std::max(list_cap, 1) * 4;
@@ -549,8 +571,8 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   std::vector<std::pair<int, int>> search_ev, solve_ev;
   std::vector<int> done_ev;
   for (long long bi = 0; bi < nbat; ++bi) {
-    const long long g0 = bi * B;
-    const int nb = (int)std::min<long long>(B, npts - g0);
+    const long long g0 = plan[bi].first;
+    const int nb = plan[bi].second;
     int *ncnt = (bi & 1) ? S.nbr_cnt2.as<int>() : S.nbr_cnt.as<int>();
     int *nidx = (bi & 1) ? S.nbr_idx2.as<int>() : S.nbr_idx.as<int>();
     hipEvent_t a, b, b2, cc, dn;

@@ -248,6 +248,29 @@ def test_c2_full_size_properties():
     assert rel <= INCR_TOL, rel
 
 
+def test_batch_plan_does_not_change_the_analysis(monkeypatch):
+    """Points are independent, so the search/solve batch plan (batch cap, short lead batch,
+    two list buffers alternating between overlapped searches and solves) must not change
+    a single bit of the analysis."""
+    from cwbl import synth
+    w = synth.make("c2", scale=0.2)
+    out = []
+    for env in ({}, {"CWBL_MAX_BATCH": "9000", "CWBL_LEAD_DIV": "8"}):
+        for key in ("CWBL_MAX_BATCH", "CWBL_LEAD_DIV"):
+            monkeypatch.delenv(key, raising=False)
+        for key, val in env.items():
+            monkeypatch.setenv(key, val)
+        _cores.clear()
+        c = core(w.k)
+        c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+        var = w.var.copy()
+        c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+        out.append(var)
+    _cores.clear()
+    assert np.isfinite(out[0]).all()
+    np.testing.assert_array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+
+
 def test_c4_full_size_properties():
     """Full C4 size (300x300x50, k=128, the 256-thread kernel): finite, bitwise reproducible
     run to run (a cross-wave LDS race once showed up only as a few NaN points that moved
