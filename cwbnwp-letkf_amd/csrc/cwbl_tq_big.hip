@@ -76,6 +76,7 @@ struct BigSmem {
   double tau[KP];
   double red[2][4][4];                    // [buffer][wave][value] of the block reductions
   double red10[4][10];                    // [wave][value]: back-transform group reduction
+  double piv[2];                          // x'_{j+1}, b1_{j+1} of the current step
   double pard;                            // sequential-sum partial handed wave to wave
   float parf;
   int ptot;
@@ -116,6 +117,15 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     b = (r[0][1] + r[1][1]) + (r[2][1] + r[3][1]);
     cc = (r[0][2] + r[1][2]) + (r[2][2] + r[3][2]);
     d = (r[0][3] + r[1][3]) + (r[2][3] + r[3][3]);
+  };
+  // one value: wave sum + the 4-entry exchange (buffers shared with bsum4's rotation)
+  auto bsum1 = [&](double a) {
+    a = wave_sum_dpp(a);
+    double(*r)[4] = sm.red[rbuf];
+    rbuf ^= 1;
+    if (lane == 0) r[wave][0] = a;
+    __syncthreads();
+    return (r[0][0] + r[1][0]) + (r[2][0] + r[3][0]);
   };
   // the reference's sequential member-order sums (member m lives in thread m), wave by wave
   auto seq_sum_f32 = [&](float x) {
@@ -333,8 +343,9 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     }
     const double x = (tid > j + 1 && tid < k) ? sm.col[tid] : 0.0;
     const double alpha = sm.col[j + 1];
-    double xn2 = x * x, z1 = 0.0, z2 = 0.0, z3 = 0.0;
-    bsum4(xn2, z1, z2, z3);
+    // x.x, x.x', x.b1 in one reduction: v = x scal + e_{j+1}, so v.u = scal (x.u) + u_{j+1}
+    double xn2 = x * x, xux = x * ux, xub = x * ub, z3 = 0.0;
+    bsum4(xn2, xux, xub, z3);
     double tau = 0.0, beta = alpha, scal = 0.0;
     if (xn2 > 0.0) {  // dlarfg, fp64 rcp/rsq refined to ~1 ulp
       const double a2 = fma(alpha, alpha, xn2);
@@ -352,6 +363,10 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     // (j = 4 bj + 3, where v vanishes on its columns) leaving exact zeros in its A v partials.
     const double v = tid == j + 1 ? 1.0 : x * scal;
     if (tid < KP) sm.vb[tid] = v;
+    if (tid == j + 1) {  // x'_{j+1}, b1_{j+1} for every thread's v.x', v.b1
+      sm.piv[0] = ux;
+      sm.piv[1] = ub;
+    }
     __syncthreads();
     double s1p = 0.0;
 #pragma unroll
@@ -390,11 +405,11 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
         s1p += sp;
       }
     }
-    double s2 = v * ux, s3 = v * ub, s1 = s1p, z4 = 0.0;
-    bsum4(s2, s3, s1, z4);  // also publishes pb (barrier inside)
-    s1 *= tau;              // p . v with p = tau A v
+    const double s2 = fma(scal, xux, sm.piv[0]), s3 = fma(scal, xub, sm.piv[1]);
     ux = fma(-tau * s2, v, ux);
     ub = fma(-tau * s3, v, ub);
+    double s1 = bsum1(s1p);  // also publishes pb (barrier inside)
+    s1 *= tau;               // p . v with p = tau A v
     double pp = 0.0;
     if (tid < KP && tid > j) {
       const double *prow = &sm.u.pb[tid >> 2][tid & 3];
