@@ -331,7 +331,9 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   double trace = 0.0;
   for (int j = 0; j < k; ++j) {
     const int J = j >> 2, qj = j & 3;
-    __syncthreads();  // previous step's readers of col are done
+    // The previous full step read col only before its four later barriers, so only the
+    // step after the (barrier-free) trailing step k-2 needs one here.
+    if (j >= k - 1) __syncthreads();
     CWBL_PUBLISH(j, sm.col);
     __syncthreads();
     const double dj = sm.col[j];
