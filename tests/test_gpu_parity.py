@@ -376,7 +376,7 @@ def test_dense_radar_c5_block_vs_oracle():
     assert rel <= INCR_TOL, rel
 
 
-@pytest.mark.parametrize("k", [80, 128])
+@pytest.mark.parametrize("k", [80, 100, 128])
 def test_large_ensemble_block_vs_oracle(k):
     """configs[3]-shaped large ensembles (k = 128, and k = 80 on the KP = 96 kernel) on a
     30x30x50 cut of the C2 grid: GPU vs the oracle on a 6x6-column block."""
