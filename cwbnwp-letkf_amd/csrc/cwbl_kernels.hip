@@ -139,71 +139,76 @@ __device__ int search_tree(const TreeDesc &T, float q0, float q1, float q2, floa
     if (!out_r2 && (count % kListGroup) != 0)
       *reinterpret_cast<int4 *>(out_idx + list_slot(count - count % kListGroup)) = grp;
   };
+  // "while-while" traversal: a lane descends internal nodes until it reaches a bucket, and
+  // the wave processes buckets together once every lane holds one (the if-if form ran the
+  // bucket loop once per subset of lanes that happened to be at a leaf).  Each lane's own
+  // visiting order, hence its result order, is unchanged.
   while (true) {
-    const TreeNode nd = nodes[node];
-    if (nd.cut_dim < 0) {  // process_terminal_node_fixedball (:1654-1707)
-      // the bucket's points are loaded four at a time ahead of the tests, so one round
-      // trip to memory covers four candidates; tests and appends stay in index order
-      for (int i0 = nd.l; i0 <= nd.u; i0 += kAhead) {
-        float4 d[kAhead];
+    TreeNode nd = nodes[node];
+    while (nd.cut_dim >= 0) {
+      const int cd = nd.cut_dim;
+      const float qval = cd == 0 ? q0 : (cd == 1 ? q1 : q2);
+      int closer, farther;
+      float dis;
+      if (qval < nd.cut_val) {
+        closer = nd.left; farther = nd.right;
+        dis = (nd.cut_val_right - qval) * (nd.cut_val_right - qval);
+      } else {
+        closer = nd.right; farther = nd.left;
+        dis = (nd.cut_val_left - qval) * (nd.cut_val_left - qval);
+      }
+      bool far_ok = farther >= 0 && dis <= r2;
+      if (far_ok) {
 #pragma unroll
-        for (int e = 0; e < kAhead; ++e)
-          d[e] = T.rdata[min(i0 + e, nd.u)];
-#pragma unroll
-        for (int e = 0; e < kAhead; ++e) {
-          const int i = i0 + e;
-          const float dx = d[e].x - q0, dy = d[e].y - q1;
-          float sd = dx * dx;
-          sd = sd + dy * dy;
-          if (dim == 3) {
-            const float dz = d[e].z - q2;
-            sd = sd + dz * dz;
-          }
-          if (i <= nd.u && sd <= r2) {
-            if (count == T.max_lz) { overflow = true; flush(); return count; }
-            if (out_r2) {  // cwbl_search: original obs index and distance
-              out_idx[count] = T.ind[i];
-              out_r2[count] = sd;
-            } else {       // analysis: the tree slot (columns are stored in slot order)
-              const int g = count % kListGroup;
-              grp.x = g == 0 ? i : grp.x;
-              grp.y = g == 1 ? i : grp.y;
-              grp.z = g == 2 ? i : grp.z;
-              grp.w = i;
-              if (g == kListGroup - 1)
-                *reinterpret_cast<int4 *>(out_idx + list_slot(count - g)) = grp;
-            }
-            ++count;
-          }
+        for (int i = 0; i < 3; ++i) {
+          if (i >= dim || i == cd || !far_ok) continue;
+          const float qi = i == 0 ? q0 : (i == 1 ? q1 : q2);
+          dis = dis + dis2_from_bnd(qi, nd.lo[i], nd.hi[i]);
+          if (dis > r2) far_ok = false;
         }
       }
-      if (sp == 0) { flush(); return count; }
-      node = stk[--sp * 64];
-      continue;
+      if (far_ok) stk[sp++ * 64] = farther;
+      node = closer;
+      nd = nodes[node];
     }
-    const int cd = nd.cut_dim;
-    const float qval = cd == 0 ? q0 : (cd == 1 ? q1 : q2);
-    int closer, farther;
-    float dis;
-    if (qval < nd.cut_val) {
-      closer = nd.left; farther = nd.right;
-      dis = (nd.cut_val_right - qval) * (nd.cut_val_right - qval);
-    } else {
-      closer = nd.right; farther = nd.left;
-      dis = (nd.cut_val_left - qval) * (nd.cut_val_left - qval);
-    }
-    bool far_ok = farther >= 0 && dis <= r2;
-    if (far_ok) {
+    // process_terminal_node_fixedball (:1654-1707): the bucket's points are loaded four at
+    // a time ahead of the tests, so one round trip to memory covers four candidates; tests
+    // and appends stay in index order
+    for (int i0 = nd.l; i0 <= nd.u; i0 += kAhead) {
+      float4 d[kAhead];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        if (i >= dim || i == cd || !far_ok) continue;
-        const float qi = i == 0 ? q0 : (i == 1 ? q1 : q2);
-        dis = dis + dis2_from_bnd(qi, nd.lo[i], nd.hi[i]);
-        if (dis > r2) far_ok = false;
+      for (int e = 0; e < kAhead; ++e)
+        d[e] = T.rdata[min(i0 + e, nd.u)];
+#pragma unroll
+      for (int e = 0; e < kAhead; ++e) {
+        const int i = i0 + e;
+        const float dx = d[e].x - q0, dy = d[e].y - q1;
+        float sd = dx * dx;
+        sd = sd + dy * dy;
+        if (dim == 3) {
+          const float dz = d[e].z - q2;
+          sd = sd + dz * dz;
+        }
+        if (i <= nd.u && sd <= r2) {
+          if (count == T.max_lz) { overflow = true; flush(); return count; }
+          if (out_r2) {  // cwbl_search: original obs index and distance
+            out_idx[count] = T.ind[i];
+            out_r2[count] = sd;
+          } else {       // analysis: the tree slot (columns are stored in slot order)
+            const int g = count % kListGroup;
+            grp.x = g == 0 ? i : grp.x;
+            grp.y = g == 1 ? i : grp.y;
+            grp.z = g == 2 ? i : grp.z;
+            grp.w = i;
+            if (g == kListGroup - 1)
+              *reinterpret_cast<int4 *>(out_idx + list_slot(count - g)) = grp;
+          }
+          ++count;
+        }
       }
     }
-    if (far_ok) stk[sp++ * 64] = farther;
-    node = closer;
+    if (sp == 0) { flush(); return count; }
+    node = stk[--sp * 64];
   }
 }
 
