@@ -179,6 +179,14 @@ int require_device() {
   return CWBL_OK;
 }
 
+// The library's streams are non-blocking: they are not ordered after work the caller has
+// queued on the null stream, on its own streams (torch's current stream) or on a
+// collective's stream (an RCCL broadcast of the obs set).  Every entry point that reads or
+// writes caller device memory therefore first waits for all of the caller's queued work, so
+// device buffers may be passed as soon as their producers have been *queued*.  (Host-memory
+// calls need no wait: the caller's host arrays are complete when the call is made.)
+hipError_t order_after_caller() { return hipDeviceSynchronize(); }
+
 // Builds the trees of one family (build_tree, module_localization.f90:35-167) and their
 // column tables.  Appends TreeDesc entries.
 int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &descs,
@@ -401,6 +409,7 @@ int cwbl_set_obs(const cwbl_obs_set *o) {
     return fail(CWBL_ERR_ARG, "bad obs set counts/pointers");
   release_obs();
   const int mem = o->memory;
+  if (mem == CWBL_MEM_DEVICE) HIPCHK(order_after_caller());
   const size_t k = (size_t)S.k;
   bool seen_g[CWBL_NUM_GTS_TYPES + 1] = {}, seen_r[CWBL_NUM_RADAR_TYPES + 1] = {};
   for (int e = 0; e < o->n_gts; ++e) {
@@ -465,6 +474,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     return fail(CWBL_ERR_ARG, "slab bounds: nx=%d ny=%d ix_lim=%d iy_lim=%d alt=%dx%d",
                 sl->nx, sl->ny, sl->ix_lim, sl->iy_lim, sl->alt_nx, sl->alt_ny);
   if (!(vp->multi_infl > 0.0f)) return fail(CWBL_ERR_ARG, "multi_infl must be > 0");
+  if (sl->memory == CWBL_MEM_DEVICE) HIPCHK(order_after_caller());
   const auto t_start = std::chrono::steady_clock::now();
   cwbl_stats st;
   std::memset(&st, 0, sizeof st);
@@ -672,6 +682,7 @@ int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const 
   const long long *doff = col_off;
   long long ncol;
   if (memory == CWBL_MEM_DEVICE) {
+    HIPCHK(order_after_caller());
     HIPCHK(hipMemcpy(&ncol, col_off + npts, 8, hipMemcpyDeviceToHost));
   } else {
     ncol = col_off[npts];
@@ -720,6 +731,7 @@ int cwbl_pack_columns(const float *global, int nx, int ny, int nz, int px, int p
     return fail(CWBL_ERR_ARG, "cwbl_pack_columns: bad arguments");
   Decomp d;
   make_decomp(d, nx, ny, nz, px, py);
+  HIPCHK(order_after_caller());
   HIPCHK(launch_pack_columns(S.stream, global, d, send));
   HIPCHK(hipStreamSynchronize(S.stream));
   return CWBL_OK;
@@ -733,6 +745,7 @@ int cwbl_unpack_columns(const float *recv, int nx, int ny, int nz, int px, int p
     return fail(CWBL_ERR_ARG, "cwbl_unpack_columns: bad arguments");
   Decomp d;
   make_decomp(d, nx, ny, nz, px, py);
+  HIPCHK(order_after_caller());
   HIPCHK(launch_unpack_columns(S.stream, recv, d, global));
   HIPCHK(hipStreamSynchronize(S.stream));
   return CWBL_OK;
@@ -747,6 +760,7 @@ int cwbl_vcoord_mean(const float *ph, long long n2d, int nz_ph, int k, int stagg
   // alpha = 1.0/(g*nmember) in default real (module_mpi_util.f90:496)
   const float gk = g * (float)k;
   const float alpha = 1.0f / gk;
+  HIPCHK(order_after_caller());
   HIPCHK(launch_vcoord_mean(S.stream, ph, n2d, nz_ph, k, stagger, alpha, alt));
   HIPCHK(hipStreamSynchronize(S.stream));
   return CWBL_OK;
@@ -756,6 +770,7 @@ int cwbl_member_sum(const float *fields, long long n, int nm, float *out) {
   if (int rc = require_device()) return rc;
   if (n < 0 || nm < 1 || (n > 0 && (!fields || !out)))
     return fail(CWBL_ERR_ARG, "cwbl_member_sum: bad arguments");
+  HIPCHK(order_after_caller());
   HIPCHK(launch_member_sum(S.stream, fields, n, nm, out));
   HIPCHK(hipStreamSynchronize(S.stream));
   return CWBL_OK;
@@ -764,6 +779,7 @@ int cwbl_member_sum(const float *fields, long long n, int nm, float *out) {
 int cwbl_scale(float *x, long long n, float alpha) {
   if (int rc = require_device()) return rc;
   if (n < 0 || (n > 0 && !x)) return fail(CWBL_ERR_ARG, "cwbl_scale: bad arguments");
+  HIPCHK(order_after_caller());
   HIPCHK(launch_scale(S.stream, x, n, alpha));
   HIPCHK(hipStreamSynchronize(S.stream));
   return CWBL_OK;

@@ -105,6 +105,30 @@ def _f4(a):
     return np.ascontiguousarray(a, dtype=np.float32)
 
 
+def check_array(a, kind, memory, name):
+    """Raise unless `a` can cross the ABI as-is: `kind` "f4" (float32) or "i4" (int32),
+    C-contiguous, a host numpy array for MEM_HOST or a device tensor for MEM_DEVICE.  The
+    library reads raw pointers (and updates the slab's var in place), so a wrong dtype,
+    stride or memory kind would otherwise be silently misread."""
+    want = {"f4": np.float32, "i4": np.int32}[kind]
+    if memory == MEM_HOST:
+        if not isinstance(a, np.ndarray):
+            raise TypeError(f"{name}: MEM_HOST needs a numpy array, got {type(a).__name__}")
+        if a.dtype != want:
+            raise TypeError(f"{name}: dtype {a.dtype}, expected {np.dtype(want)}")
+        if not a.flags.c_contiguous:
+            raise ValueError(f"{name}: not C-contiguous")
+    elif memory == MEM_DEVICE:
+        if not hasattr(a, "data_ptr") or not getattr(a, "is_cuda", False):
+            raise TypeError(f"{name}: MEM_DEVICE needs a device tensor, got {type(a).__name__}")
+        if str(a.dtype) != f"torch.{np.dtype(want).name}":
+            raise TypeError(f"{name}: dtype {a.dtype}, expected torch.{np.dtype(want).name}")
+        if not a.is_contiguous():
+            raise ValueError(f"{name}: not contiguous")
+    else:
+        raise ValueError(f"{name}: memory must be MEM_HOST or MEM_DEVICE, got {memory}")
+
+
 def _i4(a):
     return np.ascontiguousarray(a, dtype=np.int32)
 
@@ -121,24 +145,28 @@ class ObsSetBuilder:
         self.memory = memory
         self.gts, self.radar, self._keep = [], [], []
 
-    def _hold(self, a, conv):
+    def _hold(self, a, conv, name):
+        """Host arrays are converted (copied if needed); device tensors must already be of
+        the ABI's dtype and contiguous (they are passed as raw pointers)."""
         if self.memory == MEM_HOST:
             a = conv(a)
+        check_array(a, "i4" if conv is _i4 else "f4", self.memory, name)
         self._keep.append(a)
         return _ptr(a)
 
     def add_gts(self, type_id, xyz, obs, error, hdxb, qc):
         nobs = int(xyz.shape[0])
         nvar = int(obs.shape[1]) if nobs else GTS_NVAR[type_id]
-        g = GtsObs(type_id, nvar, nobs, 0, self._hold(xyz, _f4), self._hold(obs, _f4),
-                   self._hold(error, _f4), self._hold(hdxb, _f4), self._hold(qc, _i4))
+        g = GtsObs(type_id, nvar, nobs, 0, self._hold(xyz, _f4, "xyz"),
+                   self._hold(obs, _f4, "obs"), self._hold(error, _f4, "error"),
+                   self._hold(hdxb, _f4, "hdxb"), self._hold(qc, _i4, "qc"))
         self.gts.append(g)
         return self
 
     def add_radar(self, type_id, xyz, obs, hdxb):
         nobs = int(xyz.shape[0])
-        r = RadarObs(type_id, nobs, self._hold(xyz, _f4), self._hold(obs, _f4),
-                     self._hold(hdxb, _f4))
+        r = RadarObs(type_id, nobs, self._hold(xyz, _f4, "xyz"), self._hold(obs, _f4, "obs"),
+                     self._hold(hdxb, _f4, "hdxb"))
         self.radar.append(r)
         return self
 
@@ -183,7 +211,10 @@ def var_params(multi_infl=1.0, use_rtpp=0, rtpp_alpha=0.85, use_rtps=0, rtps_alp
 
 def make_slab(x, y, alt, var, ix_lim=None, iy_lim=None, memory=MEM_HOST):
     """x,y: (ny,nx); alt: (nz,alt_ny,alt_nx); var: (k,nz,ny,nx) C-order == Fortran
-    var(nx,ny,nz,0:k-1).  Host arrays must be float32 C-contiguous (var is updated in place)."""
+    var(nx,ny,nz,0:k-1).  All four must be float32 and C-contiguous, numpy arrays for MEM_HOST
+    or device tensors for MEM_DEVICE (var is updated in place, so it is never copied here)."""
+    for a, name in ((x, "x"), (y, "y"), (alt, "alt"), (var, "var")):
+        check_array(a, "f4", memory, name)
     k, nz, ny, nx = var.shape
     _, alt_ny, alt_nx = alt.shape
     s = Slab(nx, ny, nz, alt_nx, alt_ny, ix_lim if ix_lim is not None else min(nx, alt_nx),

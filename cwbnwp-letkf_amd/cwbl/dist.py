@@ -4,14 +4,18 @@ The analysis shards embarrassingly: grid columns are dealt to ranks and points n
 communicate.  The only exchange is ONE broadcast of the packed observation set from the
 rank that read it (RCCL over xGMI on MI355X, backend "nccl"; gloo on CPU for tests).  It
 replaces the reference's ibcast/iallgatherv chain (module_gts_omboma.f90:524-611,
-module_radar.f90:143-180).  Row dealing is cyclic with block 1, as the reference's
-decomposition (module_mpi_util.f90:73-188), which balances the uneven obs density.
+module_radar.f90:143-180).  Rows are dealt cyclically with block 1, which balances the
+uneven obs density.  This row-only deal is NOT the reference's decomposition: that is a
+2-D px x py cyclic column grid (letkf_local_info, module_mpi_util.f90:71-188), reproduced
+by cwbl/transpose.py for the member<->column transposes.  Points are independent, so the
+analysis does not depend on which split is used.
 """
 import numpy as np
 
 
 def shard_rows(ny, rank, world):
-    """Grid rows j owned by `rank` (cyclic, block size 1)."""
+    """Grid rows j owned by `rank`: a row-only cyclic deal (block size 1), not
+    letkf_local_info's 2-D column grid."""
     return np.arange(rank, ny, world)
 
 

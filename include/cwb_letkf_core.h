@@ -33,6 +33,10 @@
  *  - All calls are synchronous, from one host thread per process; `memory` says whether
  *    the array pointers of a struct are host pointers (copied in/out inside the call) or
  *    HIP device pointers already resident on the library's device.
+ *  - Device inputs only need to be *queued*: every call that takes device pointers first
+ *    waits for all work already queued on the device by this process (any stream: the null
+ *    stream, torch's current stream, an RCCL broadcast), and all library work on those
+ *    buffers has completed when the call returns.
  *  - Return value 0 = success; nonzero = error code, message in cwbl_last_error().
  *  - There is no CPU fallback: without a usable gfx950 device every compute entry point
  *    returns CWBL_ERR_NO_DEVICE.
@@ -83,7 +87,7 @@ enum {
 enum { CWBL_Q1_REPLICATE = 0, CWBL_Q1_PER_TYPE = 1 };
 
 typedef struct cwbl_init_params {
-  int    nmember;          /* k = config%nmember (module_config.f90:306), 2..64 */
+  int    nmember;          /* k = config%nmember (module_config.f90:306), 2..128 */
   int    device;           /* HIP device ordinal, -1 = current device */
   int    weight_function;  /* 0 Gaussian, 1 Gaspari-Cohn (module_config.f90:307) */
   float  norain_value;     /* control_nml norain_value (module_config.f90:295) */

@@ -36,3 +36,28 @@ def test_var_params_defaults_follow_module_config():
                          is_assim=[1, 0, 1])
     assert list(tp.is_assim) == [1, 0, 1, 1, 1]
     assert tp.max_lz_pts == 300
+
+
+def test_make_slab_rejects_arrays_the_abi_would_misread():
+    # the library reads raw pointers and updates var in place: wrong dtype, strides or
+    # memory kind must fail before the call
+    import pytest
+    nz, ny, nx, k = 2, 3, 4, 5
+    x = np.zeros((ny, nx), np.float32)
+    alt = np.zeros((nz, ny, nx), np.float32)
+    var = np.zeros((k, nz, ny, nx), np.float32)
+    abi.make_slab(x, x, alt, var)  # fine
+    with pytest.raises(TypeError):
+        abi.make_slab(x, x, alt, var.astype(np.float64))
+    with pytest.raises(ValueError):
+        abi.make_slab(x, x, alt, np.zeros((k, nz, nx, ny), np.float32).transpose(0, 1, 3, 2))
+    with pytest.raises(TypeError):
+        abi.make_slab(x, x, alt, var, memory=abi.MEM_DEVICE)  # host arrays as device pointers
+    b = abi.ObsSetBuilder(abi.MEM_DEVICE)
+    with pytest.raises(TypeError):
+        b.add_radar(abi.RADAR_VR, np.zeros((2, 3), np.float32), np.zeros(2, np.float32),
+                    np.zeros((k, 2), np.float32))
+    # host mode converts (copies) instead
+    abi.ObsSetBuilder().add_gts(abi.GTS_SYNOP, np.zeros((2, 3)), np.zeros((2, 5)),
+                                np.ones((2, 5)), np.zeros((k, 2, 5)),
+                                np.zeros((k, 2, 5), np.int64)).build()
