@@ -73,6 +73,74 @@ def cpu_baseline(w, target_s=12.0):
                       f"LAPACK={lib.orc_lapack_name().decode()}"}
 
 
+REF_HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+
+
+def _ref_driver_blob(w, i0, j0, nb):
+    """Input of `ref_harness driver` (oracle/ref/ref_driver.inc:54-74) for the nb x nb columns
+    at (i0, j0) of the workload: the slab in the reference's Fortran layouts and the one
+    radar type with this variable's namelist parameters (radar error rides in err_muti(1),
+    ref_driver.inc:477).  C-contiguous (.., ny, nx) arrays are Fortran (nx, ny, ..)."""
+    sub = lambda a: np.ascontiguousarray(a[..., j0:j0 + nb, i0:i0 + nb])  # noqa: E731
+    tp = w.vp.radar[w.radar_type - 1]
+    i4 = lambda v: np.asarray(v, np.int32).tobytes()  # noqa: E731
+    f4 = lambda v: np.asarray(v, np.float32).tobytes()  # noqa: E731
+    n = w.obs.shape[0]
+    return b"".join([
+        i4([w.k, nb, nb, w.nz, nb, nb, 0, w.vp.use_rtpp, w.vp.use_rtps, 1]),
+        f4([-5.0, w.vp.multi_infl, w.vp.rtpp_alpha, w.vp.rtps_alpha]),
+        f4(sub(w.x)), f4(sub(w.y)), f4(sub(w.alt)), f4(sub(w.var)),
+        i4([1, w.radar_type, 1, n, tp.use_it, tp.max_lz_pts] + list(tp.is_assim)),
+        f4([tp.hclr, tp.vclr] + list(tp.err_muti) + list(tp.err_rej)),
+        f4(w.obs_xyz), f4(w.obs), f4(w.hdxb)])
+
+
+def cpu_baseline_reference(w, target_s=12.0):
+    """The reference's own compiled code (oracle/_ref/ref_harness: letkf_solve, kdtree2 and
+    read_namelist built from /root/reference with amdflang + MKL dsyevd, the driver-loop glue
+    restated line for line) timed on the host cores as the reference runs: flat, one
+    single-threaded process per core (MPI ranks in the reference), each on its own block of
+    whole columns of the same grid.  None when the harness was not built."""
+    import subprocess
+    import tempfile
+    if not os.path.exists(REF_HARNESS):
+        return None
+    procs = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    env = dict(os.environ, MKL_CBWR="COMPATIBLE", MKL_THREADING_LAYER="SEQUENTIAL",
+               MKL_NUM_THREADS="1", OMP_NUM_THREADS="1")
+
+    def run(nb, nproc):
+        side = int(np.ceil(np.sqrt(nproc)))
+        i00, j00 = w.nx // 2 - side * nb // 2, w.ny // 2 - side * nb // 2
+        with tempfile.TemporaryDirectory() as td:
+            jobs = []
+            for p in range(nproc):
+                d = os.path.join(td, str(p))
+                os.mkdir(d)
+                with open(os.path.join(d, "in.bin"), "wb") as f:
+                    f.write(_ref_driver_blob(w, i00 + (p % side) * nb, j00 + (p // side) * nb, nb))
+                jobs.append(d)
+            t0 = time.perf_counter()
+            ps = [subprocess.Popen([REF_HARNESS, "driver", "in.bin", "out.bin"], cwd=d, env=env,
+                                   stdout=subprocess.DEVNULL) for d in jobs]
+            rcs = [p.wait() for p in ps]
+            dt = time.perf_counter() - t0
+            if any(rcs):
+                raise RuntimeError(f"ref_harness driver failed: {rcs}")
+            out = np.fromfile(os.path.join(jobs[0], "out.bin"), np.float32)
+            assert out.size == nb * nb * w.nz * w.k and np.isfinite(out).all()
+        return dt, nproc * nb * nb * w.nz
+
+    dt, pts = run(2, 1)  # one process, a 2x2-column block: the per-point time
+    nb = int(max(2, min(w.nx // int(np.ceil(np.sqrt(procs))), np.sqrt(target_s * pts / dt / w.nz))))
+    dt, pts = run(nb, procs)
+    return {"value": pts / dt, "unit": "grid-points/s", "cores": procs, "kind": "reference",
+            "sample": f"{procs} single-threaded processes (the reference's flat MPI layout), "
+                      f"each {nb}x{nb} columns x {w.nz} levels of the {w.name} grid: {pts} points "
+                      f"in {dt:.1f} s; reference letkf_solve/kdtree2/read_namelist compiled with "
+                      f"amdflang, MKL dsyevd (oracle/_ref/ref_harness driver)"}
+
+
 def time_transposes(core, w, k, rank, world, dev):
     """One letkf_scatter_grid + letkf_gather_grid of the whole variable (k members of
     nx x ny x nz fp32) through cwbl/transpose.py: HIP packing + RCCL point-to-point.
@@ -323,7 +391,13 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(w)
+            # the reference's own compiled path when it travelled with the tree (built in
+            # the container that has /root/reference), else the C restatement (port)
+            ref = cpu_baseline_reference(w)
+            port = cpu_baseline(w)
+            out["cpu_baseline"] = ref or port
+            if ref:
+                out["detail"]["cpu_baseline_port"] = port
         print(json.dumps(out), flush=True)
     core.finalize()
     if world > 1:

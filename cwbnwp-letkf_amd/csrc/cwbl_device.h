@@ -236,9 +236,11 @@ __device__ __forceinline__ float slot_r2(const f32x4 d, int dim, float q0, float
 // ---------------------------------------------------------------------------------------
 // Staged columns: E = float (converted by the consumer) or double (converted once here;
 // products of the fp32 values stay exact in fp64 either way).
-template <int KP, int CHUNK, class E = float>
+// PITCH > KP (the matrix-core assembly): a staged column also holds yo in row KP and zeros
+// in rows KP+1 .. PITCH-1, so the MFMA operand rows [Yb; yo; 0] read without selects.
+template <int KP, int CHUNK, class E = float, int PITCH = KP>
 struct ColumnChunk {
-  E yb[CHUNK][KP];
+  E yb[CHUNK][PITCH];
   E yo[CHUNK];
   unsigned long long expt[32];  // expf table (kExpT) in LDS: per-lane lookups stay on chip
 };
@@ -254,9 +256,10 @@ struct AsmLayout {
 // yo = omm * error_inv, in the reference's fp32 order; rejected columns as zeros) and calls
 // accumulate(nsl) on each staged chunk.  NT threads per point (`lane` = thread index).
 // Returns the number of accepted columns (p); with NT > 64 the count is valid in wave 0.
-template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64, class E = float, class Acc>
+template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64, class E = float, int PITCH = KP,
+          class Acc>
 __device__ __forceinline__ int stage_columns(
-    ColumnChunk<KP, CHUNK, E> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
+    ColumnChunk<KP, CHUNK, E, PITCH> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
     const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in, Acc &&accumulate) {
@@ -264,6 +267,10 @@ __device__ __forceinline__ int stage_columns(
   int ptot = 0;
   if constexpr (!ASSEMBLED) {
     if (lane < 32) ch.expt[lane] = kExpT[lane];
+    if constexpr (PITCH > KP + 1) {  // rows KP+1 .. PITCH-1 of every column stay zero
+      constexpr int NZ = PITCH - KP - 1;
+      for (int e = lane; e < CHUNK * NZ; e += NT) ch.yb[e / NZ][KP + 1 + e % NZ] = (E)0.0f;
+    }
     // other waves read the table before the chunk loop's first barrier (error_inv below);
     // LDS is not cleared between workgroups, so without this they can read a previous
     // workgroup's bytes (one wave: the lanes' LDS ops are ordered, no barrier needed)
@@ -343,7 +350,10 @@ __device__ __forceinline__ int stage_columns(
         const float w = ok ? wv : 0.0f;
         const float yo = ok ? omm * wv : 0.0f;  // omm * error_inv (:451)
         ptot += __popcll(__ballot(ok && half == 0));  // counted by wave 0
-        if (half == 0) ch.yo[sl] = (E)yo;
+        if (half == 0) {
+          ch.yo[sl] = (E)yo;
+          if constexpr (PITCH > KP) ch.yb[sl][KP] = (E)yo;
+        }
         E *dst = &ch.yb[sl][2 * VH * half];
 #pragma unroll
         for (int i = 0; i < VH; ++i) {
@@ -368,9 +378,14 @@ __device__ __forceinline__ int stage_columns(
       const int nsl = min(CHUNK, ncol - base);
       // the whole chunk is written (zeros past nsl), as on the analysis path
       if (lane < CHUNK) ch.yo[lane] = lane < nsl ? (E)yo_in[c0 + base + lane] : (E)0.0f;
-      for (int e = lane; e < CHUNK * KP; e += NT) {
-        const int s = e / KP, m = e - s * KP;
-        ch.yb[s][m] = (s < nsl && m < k) ? (E)yb_in[(c0 + base + s) * k + m] : (E)0.0f;
+      for (int e = lane; e < CHUNK * PITCH; e += NT) {
+        const int s = e / PITCH, m = e - s * PITCH;
+        E v = (E)0.0f;
+        if (s < nsl) {
+          if (m < k) v = (E)yb_in[(c0 + base + s) * k + m];
+          else if (m == KP) v = (E)yo_in[c0 + base + s];  // PITCH > KP only
+        }
+        ch.yb[s][m] = v;
       }
       __syncthreads();
       accumulate(nsl);
@@ -442,13 +457,14 @@ struct MfmaLayout {
   static constexpr int NT = (KP + 15) / 16;              // 16-row tiles per dimension
   static constexpr bool YO_ROW = KP + 1 <= 16 * NT;      // yo rides in the padding
   static constexpr int NTL = NT * (NT + 1) / 2;          // lower tiles
+  static constexpr int PITCH = YO_ROW ? 16 * NT : KP;    // staged column length
 };
 
 template <int KP, int CHUNK, bool ASSEMBLED>
 __device__ __forceinline__ void assemble_point_mfma(
-    ColumnChunk<KP, CHUNK> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
-    int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
-    const float3 pt, const long long *__restrict__ col_off,
+    ColumnChunk<KP, CHUNK, float, MfmaLayout<KP>::PITCH> &ch, const TreeDesc *__restrict__ trees,
+    const SolveConsts &c, int gi, int lane, const int *__restrict__ nbr_cnt,
+    const int *__restrict__ nbr_idx, const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in,
     f64x4 (&tile)[MfmaLayout<KP>::NTL], double &b1acc, int &ptot) {
   using L = MfmaLayout<KP>;
@@ -458,32 +474,40 @@ __device__ __forceinline__ void assemble_point_mfma(
   const int kk = lane >> 4, m = lane & 15;
   ptot = stage_columns<KP, CHUNK, ASSEMBLED>(
       ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in, [&](int nsl) {
-        // Column s = s0 + kk of the chunk feeds k-slot kk; every staged column past nsl is
-        // zero (stage_columns writes the whole chunk), so the operand reads need no
-        // predicate: row 16 I + m of tile row I is yb (row < KP), yo (row == KP) or 0.
-        // Branch-free reads, and the next 4 columns' reads are issued before this group's
-        // MFMAs, so the LDS latency hides behind the matrix pipe.
+        // Column s = 4 g + kk of the chunk feeds k-slot kk of group g; every staged column
+        // past nsl is zero (stage_columns writes the whole chunk), and with YO_ROW the
+        // staged rows are [Yb; yo; 0] up to 16 NT, so the operand reads need no predicate.
+        // The group loop is unrolled (immediate LDS offsets, static double buffer), and the
+        // next group's reads are issued before this group's MFMAs, so the LDS latency hides
+        // behind the matrix pipe.
         static_assert(CHUNK % 4 == 0, "k-slots");
-        float f[L::NT], fy;
-        auto load = [&](int s) {
+        float f[2][L::NT], fy[2];
+        auto load = [&](int b, int s) {
 #pragma unroll
           for (int I = 0; I < L::NT; ++I) {
             const int row = 16 * I + m;
-            f[I] = ch.yb[s][row < KP ? row : KP - 1];
+            if constexpr (L::YO_ROW) f[b][I] = ch.yb[s][row];
+            else f[b][I] = ch.yb[s][row < KP ? row : KP - 1];
           }
-          fy = ch.yo[s];
+          if constexpr (!L::YO_ROW) fy[b] = ch.yo[s];
         };
         const int nl = c.debug_stop == 11 ? 0 : nsl;
-        if (nl > 0) load(kk);
-        for (int s0 = 0; s0 < nl; s0 += 4) {
+        if (nl > 0) load(0, kk);
+#pragma unroll
+        for (int g = 0; g < CHUNK / 4; ++g) {
+          if (4 * g >= nl) break;  // nsl is wave-uniform
+          const int b = g & 1;
           double op[L::NT];
 #pragma unroll
           for (int I = 0; I < L::NT; ++I) {
-            const int row = 16 * I + m;
-            const float v = row < KP ? f[I] : ((L::YO_ROW && row == KP) ? fy : 0.0f);
-            op[I] = (double)v;
+            if constexpr (L::YO_ROW) {
+              op[I] = (double)f[b][I];
+            } else {
+              const int row = 16 * I + m;
+              op[I] = (double)(row < KP ? f[b][I] : 0.0f);
+            }
           }
-          if (s0 + 4 < nl) load(s0 + 4 + kk);
+          if (g + 1 < CHUNK / 4 && 4 * (g + 1) < nl) load(b ^ 1, 4 * (g + 1) + kk);
           int t = 0;
 #pragma unroll
           for (int I = 0; I < L::NT; ++I)
