@@ -101,6 +101,7 @@ struct State {
   DevBuf nbr_cnt2, nbr_idx2;                          // second list buffer (search overlap)
   hipStream_t sstream = nullptr;                      // neighbour searches of later batches
   int lead_div = 0;                                   // first batch = npts / lead_div (0: off)
+  bool serial_search = false;                         // CWBL_DEBUG_SERIAL=1: searches on S.stream
   // Points per search/solve batch.  Measured on C2 (one GPU, ms per variable): 40 k 113,
   // 70 k 110, 100 k 108, 150 k 107, 200 k 106, 500 k 109; and on an eighth of the grid (a
   // rank of the 8-GPU run): 14.7-15.0 up to 150 k, 15.3 at 200 k, 16.6 at 285 k.  Smaller
@@ -389,6 +390,8 @@ int cwbl_init(const cwbl_init_params *p) {
   if (const char *e = std::getenv("CWBL_TQ4")) S.tq4 = std::atoi(e) != 0;
   if (const char *e = std::getenv("CWBL_TQ4_SUB")) S.tq4_sub = std::atoll(e);
   if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
+  S.serial_search = false;
+  if (const char *e = std::getenv("CWBL_DEBUG_SERIAL")) S.serial_search = std::atoi(e) != 0;
   if (const char *e = std::getenv("CWBL_MAX_BATCH")) S.max_batch = std::max(256LL, std::atoll(e));
   S.inited = true;
   return CWBL_OK;
@@ -588,11 +591,14 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     hipEvent_t a, b, b2, cc, dn;
     HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b)); HIPCHK(event(ev + 2, &b2));
     HIPCHK(event(ev + 3, &cc)); HIPCHK(event(ev + 4, &dn));
-    if (bi >= 2) HIPCHK(hipStreamWaitEvent(S.sstream, S.events[done_ev[bi - 2]], 0));
-    HIPCHK(hipEventRecord(a, S.sstream));
-    HIPCHK(launch_search(S.sstream, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb, ncnt,
+    // (timing experiment: CWBL_DEBUG_SERIAL=1 runs the searches on the solve stream, so
+    // neither kernel shares the GPU with the other)
+    hipStream_t ss = S.serial_search ? S.stream : S.sstream;
+    if (bi >= 2) HIPCHK(hipStreamWaitEvent(ss, S.events[done_ev[bi - 2]], 0));
+    HIPCHK(hipEventRecord(a, ss));
+    HIPCHK(launch_search(ss, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb, ncnt,
                          nidx, nullptr, dst));
-    HIPCHK(hipEventRecord(b, S.sstream));
+    HIPCHK(hipEventRecord(b, ss));
     HIPCHK(hipStreamWaitEvent(S.stream, b, 0));
     HIPCHK(hipEventRecord(b2, S.stream));
     if (S.kp > kMaxWaveKP)

@@ -450,6 +450,17 @@ __device__ __forceinline__ void assemble_point(
 // the padding (YO_ROW), so row KP of the product is Yb d; otherwise Yb d is summed on the
 // VALU by lanes < KP.  Products of fp32 values are exact in fp64 and every tile is a
 // sequence of fp64 fused multiply-adds, like the dsyrk of the reference.
+//
+// The last tile row holds only KP+1-16(NT-1) live rows (9 at KP = 40: rows 32..39 and yo).
+// With SPLIT_LAST its tiles are not 16x16 products but NBL4 < 4 four-row strips, one
+// v_mfma_f64_4x4x4f64 each (16 cycles instead of 64 for the whole tile): its 4 blocks b
+// compute rows 4r..4r+3 of the strip against rows 4b..4b+3 of tile column J, with the strip
+// rows broadcast to every block (A lane 16k+4b+i = Y'[16(NT-1)+4r+i][k]) and tile column J
+// as B in the 16x16 operand layout itself (B lane 16k+4b+j = Y'[16J+4b+j][k]).  Its result
+// lane 16i+4b+j = (row 16(NT-1)+4r+i, col 16J+4b+j) is register r of the 16x16 tile's C/D
+// map, so the strips accumulate straight into tile registers 0..NBL4-1 (register 3 stays
+// zero: rows past yo).  At KP = 40: 9 strip MFMAs x 16 cycles instead of 3 tiles x 64 per 4
+// columns, 336 matrix-pipe cycles per 4 columns instead of 384.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 template <int KP>
@@ -458,6 +469,8 @@ struct MfmaLayout {
   static constexpr bool YO_ROW = KP + 1 <= 16 * NT;      // yo rides in the padding
   static constexpr int NTL = NT * (NT + 1) / 2;          // lower tiles
   static constexpr int PITCH = YO_ROW ? 16 * NT : KP;    // staged column length
+  static constexpr int NBL4 = YO_ROW ? (KP + 1 - 16 * (NT - 1) + 3) / 4 : 4;  // live strips
+  static constexpr bool SPLIT_LAST = NBL4 < 4;
 };
 
 template <int KP, int CHUNK, bool ASSEMBLED>
@@ -481,13 +494,18 @@ __device__ __forceinline__ void assemble_point_mfma(
         // next group's reads are issued before this group's MFMAs, so the LDS latency hides
         // behind the matrix pipe.
         static_assert(CHUNK % 4 == 0, "k-slots");
-        float f[2][L::NT], fy[2];
+        constexpr int NS = L::SPLIT_LAST ? L::NBL4 : 1;
+        float f[2][L::NT], fy[2], fs[2][NS];
         auto load = [&](int b, int s) {
 #pragma unroll
           for (int I = 0; I < L::NT; ++I) {
             const int row = 16 * I + m;
             if constexpr (L::YO_ROW) f[b][I] = ch.yb[s][row];
             else f[b][I] = ch.yb[s][row < KP ? row : KP - 1];
+          }
+          if constexpr (L::SPLIT_LAST) {  // strip rows, broadcast over the 4 blocks
+#pragma unroll
+            for (int r = 0; r < NS; ++r) fs[b][r] = ch.yb[s][16 * (L::NT - 1) + 4 * r + (m & 3)];
           }
           if constexpr (!L::YO_ROW) fy[b] = ch.yo[s];
         };
@@ -507,13 +525,23 @@ __device__ __forceinline__ void assemble_point_mfma(
               op[I] = (double)(row < KP ? f[b][I] : 0.0f);
             }
           }
+          double os[NS];
+#pragma unroll
+          for (int r = 0; r < NS; ++r) os[r] = L::SPLIT_LAST ? (double)fs[b][r] : 0.0;
           if (g + 1 < CHUNK / 4 && 4 * (g + 1) < nl) load(b ^ 1, 4 * (g + 1) + kk);
           int t = 0;
 #pragma unroll
           for (int I = 0; I < L::NT; ++I)
 #pragma unroll
-            for (int J = 0; J <= I; ++J, ++t)
-              tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[I], op[J], tile[t], 0, 0, 0);
+            for (int J = 0; J <= I; ++J, ++t) {
+              if (L::SPLIT_LAST && I == L::NT - 1) {
+#pragma unroll
+                for (int r = 0; r < NS; ++r)
+                  tile[t][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(os[r], op[J], tile[t][r], 0, 0, 0);
+              } else {
+                tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[I], op[J], tile[t], 0, 0, 0);
+              }
+            }
         }
         if constexpr (!L::YO_ROW) {
           for (int s = 0; s < nsl; ++s)
