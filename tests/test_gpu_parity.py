@@ -147,6 +147,38 @@ def test_device_memory_path_equals_host_path():
     np.testing.assert_array_equal(got.view(np.uint32), hvar.view(np.uint32))
 
 
+def test_device_inputs_only_need_to_be_queued():
+    """cwbl_set_obs / cwbl_analyze_var on device buffers whose producers are still queued
+    (behind a GPU spin on a side stream): the library orders itself after them."""
+    torch = pytest.importorskip("torch")
+    case = DriverCase("driver_mixed.npz")
+    c = core(case.k, case.wf, case.norain)
+    dev = torch.device("cuda:0")
+    s = torch.cuda.Stream()
+    staged = []
+
+    def late(a):  # a device copy of `a` written only after ~10 ms of GPU spin on stream s
+        src = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        dst = torch.zeros_like(src)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(20_000_000)
+            dst.copy_(src)
+        staged.append(src)
+        return dst
+
+    c.set_obs(case.obs_set(memory=abi.MEM_DEVICE, to_device=late))
+    x, y, alt = (late(np.asarray(a, np.float32)) for a in (case.x, case.y, case.alt))
+    var = late(np.asarray(case.var_in, np.float32).copy())
+    slab = abi.make_slab(x, y, alt, var, case.ix_lim, case.iy_lim, memory=abi.MEM_DEVICE)
+    c.analyze_var(case.vp, slab)
+    got = var.cpu().numpy()
+    c.set_obs(case.obs_set())
+    hslab, hvar = case.slab()
+    c.analyze_var(case.vp, hslab)
+    np.testing.assert_array_equal(got.view(np.uint32), hvar.view(np.uint32))
+
+
 def test_analyze_before_set_obs_is_a_state_error():
     c = abi.Core(8, device=0)
     _cores.clear()

@@ -48,6 +48,34 @@ def test_pack_unpack_vs_oracle(nz, ny, nx, world):
     assert torch.equal(back, f)
 
 
+@pytest.mark.parametrize("side_stream", [False, True])
+def test_device_inputs_only_need_to_be_queued(side_stream):
+    """The library's streams are non-blocking; every device-pointer entry point must wait for
+    work the caller has merely queued (a NaN fill queued on torch's stream landed
+    after unpack_columns had written its output).  The producer here is held back by a GPU
+    spin, on torch's current stream or on a side stream, and the library is called at once."""
+    c = core()
+    nz, ny, nx, world = 4, 33, 65, 12
+    px, py = tr.dims_create(world)
+    g = torch.randn((nz, ny, nx), device="cuda", dtype=torch.float32)
+    f = torch.zeros_like(g)
+    send = torch.zeros((nz * ny * nx,), device="cuda")
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream() if side_stream else torch.cuda.current_stream()
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(20_000_000)  # ~10 ms of GPU spin before the input is written
+        f.copy_(g)
+    c.pack_columns(f, nx, ny, nz, px, py, send)  # no synchronize in between
+    np.testing.assert_array_equal(send.cpu().numpy(), mo.pack_columns(g.cpu().numpy(), px, py))
+    back = torch.full_like(g, float("nan"))  # queued on torch's stream, after the call above
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(20_000_000)
+        back.fill_(float("nan"))
+    c.unpack_columns(send, nx, ny, nz, px, py, back)
+    torch.cuda.synchronize()
+    assert torch.equal(back, g)
+
+
 @pytest.mark.parametrize("k,stagger", [(8, 0), (40, 0), (40, 1), (128, 0)])
 def test_vcoord_mean_vs_oracle(k, stagger):
     c = core()
