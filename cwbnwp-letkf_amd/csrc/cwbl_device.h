@@ -299,6 +299,7 @@ __device__ __forceinline__ int stage_columns(
       // correction each way (nvar is wave-uniform; 1 for radar)
       const float rnv = 1.0f / (float)nvar;
       auto divn = [&](int q) {
+        if (nvar == 1) return q;  // radar (wave-uniform): no division
         int j = (int)((float)q * rnv);
         j -= j * nvar > q ? 1 : 0;
         j += (j + 1) * nvar <= q ? 1 : 0;
