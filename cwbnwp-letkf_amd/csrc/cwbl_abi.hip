@@ -116,6 +116,8 @@ struct State {
   bool jacobi = false;                                // CWBL_SOLVER=jacobi: eigen path
   bool tq4 = true;                                    // CWBL_TQ4=0: one-kernel KP=40 solve
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: hand-off batch (points)
+  bool big_split = true;                              // CWBL_BIG_SPLIT=0: one-kernel KP=128 solve
+  long long big_sub = 32768;                          // CWBL_BIG_SUB: KP=128 hand-off batch
   std::vector<hipEvent_t> events;
 };
 
@@ -333,6 +335,7 @@ SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps,
   c.quad = S.quad.as<double2>();
   if (const char *e = std::getenv("CWBL_DEBUG_TQ_STOP")) c.debug_stop = std::atoi(e);
   if (const char *e = std::getenv("CWBL_DEBUG_STAGGER")) c.stagger = std::atoi(e);
+  if (const char *e = std::getenv("CWBL_DEBUG_TQ_STEPS")) c.debug_steps = std::atoi(e);
   return c;
 }
 
@@ -389,6 +392,10 @@ int cwbl_init(const cwbl_init_params *p) {
   S.tq4 = true;
   if (const char *e = std::getenv("CWBL_TQ4")) S.tq4 = std::atoi(e) != 0;
   if (const char *e = std::getenv("CWBL_TQ4_SUB")) S.tq4_sub = std::atoll(e);
+  S.big_split = true;
+  S.big_sub = 32768;
+  if (const char *e = std::getenv("CWBL_BIG_SPLIT")) S.big_split = std::atoi(e) != 0;
+  if (const char *e = std::getenv("CWBL_BIG_SUB")) S.big_sub = std::max(64LL, std::atoll(e));
   if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
   S.serial_search = false;
   if (const char *e = std::getenv("CWBL_DEBUG_SERIAL")) S.serial_search = std::atoi(e) != 0;
@@ -601,7 +608,22 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     HIPCHK(hipEventRecord(b, ss));
     HIPCHK(hipStreamWaitEvent(S.stream, b, 0));
     HIPCHK(hipEventRecord(b2, S.stream));
-    if (S.kp > kMaxWaveKP)
+    if (S.kp == kBigSplitKP && S.big_split && S.k > kBigJ0 + 2) {
+      // 256-thread assembly + first kBigJ0 steps -> workspace -> one-wavefront tail, in
+      // hand-off batches of Bs points (a multiple of kListLanes; ~100 KB per point)
+      const long long nsub = (nb + S.big_sub - 1) / S.big_sub;
+      long long Bs = (nb + nsub - 1) / nsub;
+      Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
+      HIPCHK(S.wsa.ensure((size_t)Bs * BigHandoff<kBigSplitKP, kBigJ0>::WORDS * 8));
+      for (long long s0 = 0; s0 < nb; s0 += Bs) {
+        const int ns = (int)std::min<long long>(Bs, nb - s0);
+        HIPCHK(launch_big_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,
+                                  nidx + s0 * list_cap, S.info.as<int2>() + s0,
+                                  S.wsa.as<double>()));
+        HIPCHK(launch_solve_tqb_tail(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
+                                     S.info.as<int2>() + s0));
+      }
+    } else if (S.kp > kMaxWaveKP)
       HIPCHK(launch_solve_tq_big(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
                                  nullptr, nullptr, nullptr, nullptr, nullptr,
                                  S.info.as<int2>()));

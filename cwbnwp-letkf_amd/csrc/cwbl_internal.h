@@ -71,6 +71,8 @@ struct SolveConsts {
   int   stagger;              // CWBL_DEBUG_STAGGER: start-phase offset unit in cycles (experiment)
   int   debug_stop;           // CWBL_DEBUG_TQ_STOP: 1 = after assembly, 2 = after
                               // tridiagonalisation, 3 = after quadrature (timing ablation only)
+  int   debug_steps;          // CWBL_DEBUG_TQ_STEPS: > 0 runs only that many Householder steps
+                              // in solve_tq_big_kernel (timing ablation only)
 };
 
 // Inverse-square-root quadrature of solve_tq_kernel (quad_tables.cpp): level L = 1..12
@@ -169,6 +171,34 @@ hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees,
                                    const int *nbr_idx, int2 *info, double *ws);
 hipError_t launch_solve_tq4(hipStream_t s, int kp, SolveConsts c, SlabDev slab, long long g0,
                             int npts, const double *ws, int2 *info);
+
+// Split form of the KP = 128 slab path (configs[3]: k = 97..128).  solve_tq_big_kernel<128,
+// false, kBigJ0> assembles A and runs the first kBigJ0 Householder steps (4x4 register
+// blocks over 256 threads, one point per workgroup), then hands the trailing
+// (KP-J0)^2 matrix, its J0 reflectors, T so far and Q^T b1, Q^T x' over through the
+// workspace (BigHandoff, info[gi] = (p, 0)); solve_tqb_tail_kernel (cwbl_tq_tail.hip)
+// finishes with one point per wavefront, lane l holding the full trailing row J0 + l.
+constexpr int kBigSplitKP = 128;
+constexpr int kBigJ0 = 64;
+// fp64 words of one point's hand-off record
+template <int KP, int J0>
+struct BigHandoff {
+  static constexpr int KT = KP - J0;        // trailing rows
+  static constexpr int TA = 0;              // trailing A, full: (r, c) at TA + c*KT + r
+  static constexpr int HV = TA + KT * KT;   // reflector j < J0 at HV + j*KP + row (rows > j)
+  static constexpr int D = HV + J0 * KP;    // d_0 .. d_{J0-1}
+  static constexpr int E = D + J0;          // c(j, j+1), j = 0..J0-1
+  static constexpr int TAU = E + J0;        // tau_0 .. tau_{J0-1}
+  static constexpr int U1 = TAU + J0;       // Q_J0^T b1 (KP)
+  static constexpr int U2 = U1 + KP;        // Q_J0^T x' (KP)
+  static constexpr int BT = U2 + KP;        // tail scratch: its reflector rows (KT x KT)
+  static constexpr int WORDS = BT + KT * KT;
+};
+hipError_t launch_big_handoff(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
+                              SlabDev slab, long long g0, int npts, const int *nbr_cnt,
+                              const int *nbr_idx, int2 *info, double *ws);
+hipError_t launch_solve_tqb_tail(hipStream_t s, int kp, SolveConsts c, SlabDev slab,
+                                 long long g0, int npts, double *ws, int2 *info);
 
 // KP = 96, 128: one 256-thread workgroup per point (cwbl_tq_big.hip)
 hipError_t launch_solve_tq_big(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,

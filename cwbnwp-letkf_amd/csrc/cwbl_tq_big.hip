@@ -82,14 +82,16 @@ struct BigSmem {
   int ptot;
 };
 
-template <int KP, bool ASSEMBLED>
+// HS > 0 (slab path, KP = kBigSplitKP): stop after HS Householder steps and hand the rest
+// over through ws (BigHandoff<KP, HS>) to solve_tqb_tail_kernel.
+template <int KP, bool ASSEMBLED, int HS = 0>
 __global__ void __launch_bounds__(kBigThreads)
 solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
                     long long g0, int npts, const int *__restrict__ nbr_cnt,
                     const int *__restrict__ nbr_idx, const long long *__restrict__ col_off,
                     const float *__restrict__ yo_in, const float *__restrict__ yb_in,
                     const float *__restrict__ xb_in, float *__restrict__ xa_out,
-                    int2 *__restrict__ info) {
+                    int2 *__restrict__ info, double *__restrict__ ws = nullptr) {
   constexpr int NT = kBigThreads;
   constexpr int H = KP / 2;
   using L = AsmLayout<KP, NT>;
@@ -329,7 +331,10 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
 
   // ---- Householder tridiagonalisation ----------------------------------------------------
   double trace = 0.0;
-  for (int j = 0; j < k; ++j) {
+  static_assert(HS == 0 || (!ASSEMBLED && HS % 4 == 0 && HS + 4 <= KP), "hand-off step");
+  // (k > HS + 2 on the split path: every hand-off step is a full step)
+  const int jend = HS > 0 ? HS : c.debug_steps > 0 ? min(k, c.debug_steps) : k;
+  for (int j = 0; j < jend; ++j) {
     const int J = j >> 2, qj = j & 3;
     // The previous full step read col only before its four later barriers, so only the
     // step after the (barrier-free) trailing step k-2 needs one here.
@@ -462,6 +467,55 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
         }
       }
     }
+  }
+  if constexpr (HS > 0) {  // hand-off (BigHandoff) after HS steps
+    using HO = BigHandoff<KP, HS>;
+    constexpr int KT = HO::KT, JB = HS / 4;
+    double *__restrict__ w = ws + (long long)gi * HO::WORDS;
+    __syncthreads();  // T, tau of the last steps are in LDS
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) {
+      if (tid + NT * it < NBLK) {
+        if (bj[it] >= JB) {  // trailing block: both triangles of the full KT x KT matrix
+          const int a0 = 4 * (bi[it] - JB), b0 = 4 * (bj[it] - JB);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // column b0 + q, rows a0 .. a0 + 3
+            double *d = w + HO::TA + (b0 + q) * KT + a0;
+            pub4(d, acc[it][q], acc[it][4 + q], acc[it][8 + q], acc[it][12 + q]);
+          }
+          if (bi[it] != bj[it]) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {  // column a0 + r, rows b0 .. b0 + 3
+              double *d = w + HO::TA + (a0 + r) * KT + b0;
+              pub4(d, acc[it][4 * r], acc[it][4 * r + 1], acc[it][4 * r + 2], acc[it][4 * r + 3]);
+            }
+          }
+        } else {  // reflector columns j = 4 bj + q: v_j at rows > j (1 at row j + 1)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int j = 4 * bj[it] + q, a0 = 4 * bi[it];
+            double e[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int a = a0 + r;
+              e[r] = a == j + 1 ? 1.0 : a > j + 1 ? acc[it][4 * r + q] : 0.0;
+            }
+            pub4(w + HO::HV + j * KP + a0, e[0], e[1], e[2], e[3]);
+          }
+        }
+      }
+    }
+    if (tid < KP) {
+      w[HO::U1 + tid] = ub;
+      w[HO::U2 + tid] = ux;
+    }
+    if (tid < HS) {
+      w[HO::D + tid] = sm.tq[tid][0];
+      w[HO::E + tid] = sm.tq[tid + 1][1];
+      w[HO::TAU + tid] = sm.tau[tid];
+    }
+    if (tid == 0) info[gi] = make_int2(ptot, 0);
+    return;
   }
   if (tid < KP) {
     sm.tq[tid][2] = ub;
@@ -673,6 +727,17 @@ static hipError_t launch_big_kp(hipStream_t s, bool assembled, const TreeDesc *t
     hipLaunchKernelGGL((solve_tq_big_kernel<KP, false>), dim3(npts), dim3(kBigThreads), 0, s,
                        trees, c, slab, g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa,
                        info);
+  return hipGetLastError();
+}
+
+hipError_t launch_big_handoff(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
+                              SlabDev slab, long long g0, int npts, const int *nbr_cnt,
+                              const int *nbr_idx, int2 *info, double *ws) {
+  if (npts <= 0) return hipSuccess;
+  if (kp != kBigSplitKP || c.k <= kBigJ0 + 2) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((solve_tq_big_kernel<kBigSplitKP, false, kBigJ0>), dim3(npts),
+                     dim3(kBigThreads), 0, s, trees, c, slab, g0, npts, nbr_cnt, nbr_idx,
+                     nullptr, nullptr, nullptr, nullptr, nullptr, info, ws);
   return hipGetLastError();
 }
 

@@ -1,0 +1,379 @@
+// cwbl_tq_tail.hip — solve_tqb_tail_kernel<KP, J0>: the second half of the per-point LETKF
+// solve (letkf_solve, module_letkf_core.f90:598-700) for large ensembles (configs[3],
+// k = 97..128), one grid point per wavefront.
+//
+// solve_tq_big_kernel<KP, false, J0> (cwbl_tq_big.hip) stages the point's columns, assembles
+// A = (k-1)/infl I + Yb Yb^T and b1 = Yb d on the matrix cores and runs the first J0 steps of
+// the Householder tridiagonalisation A = Q T Q^T (dsytd2 order) on 4x4 register blocks spread
+// over a 256-thread workgroup; each of its steps is a chain of five barriers and LDS
+// exchanges, so its cost per step is nearly fixed.  It hands the trailing KT x KT matrix,
+// its J0 reflectors, T so far and Q^T b1, Q^T x' over through the workspace (BigHandoff).
+// This kernel finishes the algorithm — the remaining steps, the T^-1/2 quadrature and the
+// T^-1 solve, the back-transform and the RTPP/RTPS epilogue in the reference's fp32 order —
+// inside one wavefront, with no barrier between lanes of different waves:
+//
+//   lane l holds the FULL trailing row J0 + l (KT = 64 doubles, static register indices)
+//   and the vectors' rows l (prefix) and J0 + l (trailing).
+//
+// A step needs the pivot column per lane and the pivot row as wave-uniform values.  A is
+// kept symmetric (both triangles are updated), so column j is row j: lane j writes its row
+// to LDS once per step (each lane then reads its own entry), and the matvec and the rank-2
+// update take x_c = A(j, c) and w_c straight from lanes j and c (v_readlane).  Row j is
+// never touched again by later steps (v and w vanish there), so after the step it IS the
+// Householder vector (v = scal x, 1 at row j + 1): the back-transform reads it from there.
+// Columns are processed in groups of eight; a group left of the pivot is skipped by a
+// uniform branch, the group holding column j + 1 selects its operands on the scalar unit.
+#include "cwbl_device.h"
+
+#include <utility>
+
+namespace cwbl {
+
+namespace {
+
+template <int... Is, class F>
+__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, Is...>, F &&f) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>), in order
+template <int N, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+  sfor_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+__device__ __forceinline__ float readlane_f32(float x, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
+}
+
+}  // namespace
+
+template <int KP, int J0>
+struct TailSmem {
+  static constexpr int KT = KP - J0;
+  double row[KT];         // the pivot row of the step (= its column) / a reflector
+  double tq[KP + 1][4];   // d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
+  double tau[KP];
+  double scl[KP];         // this kernel's reflectors: v = scl * x below row j + 1
+  double Ym[KP], Zm[KP];  // quadrature sum / exact solve, walk order
+};
+
+// WPE: waves per SIMD the register budget is sized for (2: 256 VGPRs, 3: 168)
+template <int KP, int J0, int WPE>
+__global__ void __launch_bounds__(64, WPE)
+solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
+                      double *__restrict__ ws, int2 *__restrict__ info) {
+  using HO = BigHandoff<KP, J0>;
+  constexpr int KT = HO::KT;  // trailing rows: one per lane
+  constexpr int H = KP / 2;   // rows walked by each side of a twisted solve
+  constexpr int NG = KT / 8;  // column groups
+  static_assert(KT == 64 && J0 == 64, "one trailing row and one prefix row per lane");
+  using SM = TailSmem<KP, J0>;
+  __shared__ SM sm;
+
+  const int gi = xcd_remap(blockIdx.x, gridDim.x);  // the hand-off kernel's point of block b
+  if (gi >= npts) return;
+  const int l = threadIdx.x;
+  const int k = c.k;
+  const int ptot = info[gi].x;
+  if (ptot == 0) return;  // no accepted observation: var unchanged (:220, :226)
+  const auto *__restrict__ w = gptr(ws + (long long)gi * HO::WORDS);
+
+  // ---- hand-off: trailing rows (coalesced by column), T and the vectors' prefix ----------
+  double A[KT];
+  sfor<KT>([&](auto cc) {
+    constexpr int col = decltype(cc)::value;
+    A[col] = w[HO::TA + col * KT + l];
+  });
+  double u1t = w[HO::U1 + J0 + l], u2t = w[HO::U2 + J0 + l];  // trailing Q^T b1, Q^T x'
+  sm.tq[l][0] = w[HO::D + l];
+  sm.tq[l + 1][1] = w[HO::E + l];
+  sm.tq[l][2] = w[HO::U1 + l];
+  sm.tq[l][3] = w[HO::U2 + l];
+  sm.tau[l] = w[HO::TAU + l];
+  // trailing rows of T: decoupled unit rows until the steps write them (rows >= k stay so)
+  sm.tq[J0 + l][0] = 1.0;
+  sm.tq[J0 + l + 1][1] = 0.0;
+  sm.tau[J0 + l] = 0.0;
+  if (l == 0) sm.tq[0][1] = 0.0;
+  __syncthreads();
+  double trace = 0.0;  // d_0 + d_1 + ... in step order, as solve_tq_big_kernel sums it
+  for (int j = 0; j < J0; ++j) trace += sm.tq[j][0];
+
+  // lane jl's row -> sm.row (static register indices); with `park`, also to the record's
+  // scratch rows (BT), where the back-transform finds it once the registers are released
+  double *__restrict__ parked = ws + (long long)gi * HO::WORDS + HO::BT;
+  auto publish_row = [&](int jl, bool park) {
+    __syncthreads();  // the previous readers of sm.row are done
+    if (l == jl) {
+      sfor<KT / 2>([&](auto cc) {
+        constexpr int col = 2 * decltype(cc)::value;
+        const double2 p2 = make_double2(A[col], A[col + 1]);
+        *reinterpret_cast<double2 *>(&sm.row[col]) = p2;
+        if (park) *reinterpret_cast<double2 *>(&parked[jl * KT + col]) = p2;
+      });
+    }
+    __syncthreads();
+  };
+
+  // ---- Householder steps j = J0 .. k-3 (local jl = j - J0) --------------------------------
+  const int nst = k - 2 - J0;  // k > J0 + 2 (launcher)
+  for (int jl = 0; jl < nst; ++jl) {
+    const int j = J0 + jl, j1 = jl + 1;
+    publish_row(jl, true);
+    const double dj = sm.row[jl], alpha = sm.row[j1];
+    const double xr = sm.row[l];  // A(J0 + l, j)
+    trace += dj;
+    const double x = l > j1 ? xr : 0.0;
+    double xx = x * x, xu = x * u2t, xb = x * u1t, z3 = 0.0;
+    wave_sum4_dpp(xx, xu, xb, z3);
+    // dlarfg with fp64 rcp/rsq refined to ~1 ulp; H = I when x = 0 (tau = 0, v = e_j+1)
+    const double a2 = fma(alpha, alpha, xx);
+    const double rs = rsq64(a2);  // 1/|beta|
+    const bool nz = xx > 0.0;
+    const double bt = -copysign(a2 * rs, alpha);
+    const double beta = nz ? bt : alpha;
+    const double tau = nz ? (bt - alpha) * -copysign(rs, alpha) : 0.0;
+    const double rab = rcp64(alpha - bt);
+    const double scal = nz ? rab : 0.0;
+    if (l == 0) {
+      sm.tq[j][0] = dj;
+      sm.tq[j + 1][1] = beta;
+      sm.tau[j] = tau;
+      sm.scl[j] = scal;
+    }
+    const double v = l == j1 ? 1.0 : x * scal;
+    const double s2 = fma(scal, xu, readlane_f64(u2t, j1));  // v . x'
+    const double s3 = fma(scal, xb, readlane_f64(u1t, j1));  // v . b1
+    u2t = fma(-tau * s2, v, u2t);
+    u1t = fma(-tau * s3, v, u1t);
+
+    // The uniform side of v: v_c = scal * xt_c with xt_c = x_c = A(j, c) below row j + 1 and
+    // xt_{j+1} = alpha - beta = 1/scal (0 when H = I), so column j + 1 needs no special
+    // case (v_{j+1} = scal (alpha - beta) is 1 to the last bit or so).
+    const double amb = nz ? alpha - bt : 0.0;
+    // A v = scal * sum_{c >= j+1} A(:, c) xt_c; x_c from lane jl, a group's eight broadcasts
+    // first (16 SGPRs), then its FMAs; groups left of column j + 1 are skipped
+    double q0 = 0.0, q1 = 0.0;
+    sfor<NG>([&](auto gg) {
+      constexpr int c0 = 8 * decltype(gg)::value;
+      if (c0 + 7 >= j1) {
+        double xs[8];
+        sfor<8>([&](auto ii) { xs[ii] = readlane_f64(A[c0 + ii], jl); });
+        sfor<8>([&](auto ii) {
+          constexpr int col = c0 + decltype(ii)::value;
+          const double xt = col > j1 ? xs[ii] : col == j1 ? amb : 0.0;  // scalar selects
+          if constexpr (col % 2 == 0) q0 = fma(A[col], xt, q0);
+          else q1 = fma(A[col], xt, q1);
+        });
+      }
+    });
+    const double av = scal * (q0 + q1);             // (A v)_l
+    const double s1 = tau * wave_sum_dpp(v * av);   // v^T (tau A v); v = 0 at rows <= j
+    const double wl = l > jl ? fma(-0.5 * tau * s1, v, tau * av) : 0.0;
+    const double wsl = wl * scal;
+    // A <- A - v w^T - w v^T; xt_c from the published row (LDS broadcast), w_c from lane c
+    sfor<NG>([&](auto gg) {
+      constexpr int c0 = 8 * decltype(gg)::value;
+      if (c0 + 7 >= j1) {
+        double wc[8], xs[8];
+        sfor<8>([&](auto ii) { wc[ii] = readlane_f64(wl, c0 + ii); });
+        sfor<4>([&](auto ii) {
+          const double2 x2 = *reinterpret_cast<const double2 *>(&sm.row[c0 + 2 * ii]);
+          xs[2 * ii] = x2.x;
+          xs[2 * ii + 1] = x2.y;
+        });
+        if (c0 > j1) {
+          sfor<8>([&](auto ii) {
+            constexpr int col = c0 + decltype(ii)::value;
+            A[col] = fma(-v, wc[ii], fma(-wsl, xs[ii], A[col]));
+          });
+        } else {  // the group of column j + 1
+          sfor<8>([&](auto ii) {
+            constexpr int col = c0 + decltype(ii)::value;
+            const double xt = col > j1 ? xs[ii] : col == j1 ? amb : 0.0;
+            A[col] = fma(-v, wc[ii], fma(-wsl, xt, A[col]));
+          });
+        }
+      }
+    });
+  }
+  {  // the trailing 2x2 (rows k-2, k-1): already tridiagonal
+    const int jl = nst;
+    publish_row(jl, false);
+    const double d0 = sm.row[jl], e1 = sm.row[jl + 1];
+    publish_row(jl + 1, false);
+    const double d1 = sm.row[jl + 1];
+    trace += d0;
+    trace += d1;
+    if (l == 0) {
+      sm.tq[k - 2][0] = d0;
+      sm.tq[k - 1][1] = e1;
+      sm.tq[k - 1][0] = d1;
+    }
+  }
+  sm.tq[J0 + l][2] = u1t;
+  sm.tq[J0 + l][3] = u2t;
+  __syncthreads();
+
+  // ---- T^-1/2 u2 by quadrature, u1^T T^-1 u2 exactly (solve_tq_big_kernel's rule) --------
+  // lane = node (0..31) + 32 side: side 0 walks rows 0..H-1, side 1 rows KP-1..H; node 31
+  // solves T^-1 u2.  The forward sweep is checkpointed every 8 rows and recomputed per
+  // segment in the backward sweep.
+  const double m = (double)c.inflat;
+  const double ratio = trace / m - (double)(k - 1);
+  int level = 1;
+  double dec = 10.0;
+  while (level < kQuadLevels && dec < ratio) {
+    dec *= 10.0;
+    ++level;
+  }
+  {
+    const int node = l & 31, side = l >> 5;
+    double sigma = 0.0, omega = 0.0;
+    if (node < kQuadNodes) {
+      const double2 tw = c.quad[(level - 1) * 32 + node];
+      sigma = m * tw.x;
+      omega = sqrt(m) * tw.y;
+    }
+    const int dir = side ? -4 : 4;
+    const double *q = &sm.tq[side ? KP - 1 : 0][0];
+    const int cs = side ? 5 : 1;  // coupling with the previous row of the walk
+    auto fwd = [&](int t, double &dl, double &gt) {
+      const double *qt = q + dir * t;
+      const double ct = qt[cs];
+      const double lt = ct * rcp64(dl);
+      dl = fma(-lt, ct, qt[0] + sigma);
+      gt = fma(-lt, gt, qt[3]);
+    };
+    constexpr int S = 8, NS = H / S;
+    double ckd[NS], ckg[NS];
+    double dl = q[0] + sigma, gt = q[3];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      ckd[s] = dl;
+      ckg[s] = gt;
+#pragma unroll
+      for (int t = S * s + 1; t < S * s + S; ++t) fwd(t, dl, gt);
+      if (s + 1 < NS) fwd(S * s + S, dl, gt);
+    }
+    const double cm = sm.tq[H][1];  // meeting rows H-1 (top) and H (bottom)
+    const double dlo = __shfl_xor(dl, 32, 64), go = __shfl_xor(gt, 32, 64);
+    double xv = (gt * dlo - cm * go) / fma(dl, dlo, -cm * cm);
+    double *ym = sm.Ym + side * H, *zm = sm.Zm + side * H;
+    for (int s = NS - 1; s >= 0; --s) {
+      double hh[S], mmv[S];
+      double d2 = ckd[s], g2 = ckg[s];
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        const int t = S * s + i;
+        if (i > 0) fwd(t, d2, g2);
+        const double rd = rcp64(d2);
+        hh[i] = g2 * rd;
+        mmv[i] = (t + 1 < H) ? q[dir * (t + 1) + cs] * rd : 0.0;  // c_{t+1} / dl_t
+      }
+#pragma unroll
+      for (int i = S - 1; i >= 0; --i) {
+        const int t = S * s + i;
+        if (t != H - 1) xv = fma(-mmv[i], xv, hh[i]);
+        const double ys = half_sum_dpp(omega * xv);
+        if (node == 0) ym[t] = ys;
+        if (node == 31) zm[t] = xv;
+      }
+    }
+  }
+  __syncthreads();
+  // rows l (slot 0) and J0 + l (slot 1) in walk order: side 1 walks KP-1 .. H
+  const int w1 = H + (KP - 1 - (J0 + l));
+  double y0 = sm.Ym[l], y1 = sm.Ym[w1];
+  const double d = wave_sum_dpp(fma(sm.tq[l][2], sm.Zm[l], sm.tq[J0 + l][2] * sm.Zm[w1]));
+
+  // ---- back-transform y <- Q y = H_0 H_1 ... H_{k-3} y ------------------------------------
+  for (int jl = nst - 1; jl >= 0; --jl) {  // this kernel's reflectors: the parked rows
+    const int j1 = jl + 1;
+    const double xr = parked[jl * KT + l];
+    const double vv = l == j1 ? 1.0 : (l > j1 ? sm.scl[J0 + jl] * xr : 0.0);
+    const double a = wave_sum_dpp(vv * y1);
+    y1 = fma(-sm.tau[J0 + jl] * a, vv, y1);
+  }
+#pragma unroll 4
+  for (int j = J0 - 1; j >= 0; --j) {  // the hand-off's reflectors (rows > j)
+    const double h0 = w[HO::HV + j * KP + l], h1 = w[HO::HV + j * KP + J0 + l];
+    const double v0 = l > j ? h0 : 0.0;  // row j + 1 holds 1.0
+    const double a = wave_sum_dpp(fma(v0, y0, h1 * y1));
+    const double ta = sm.tau[j] * a;
+    y0 = fma(-ta, v0, y0);
+    y1 = fma(-ta, h1, y1);
+  }
+
+  // ---- analysis and RTPP / RTPS (:671-698), fp32 in the reference's order -----------------
+  long long P = 0;
+  {
+    const long long g = g0 + gi;
+    const int i = (int)(g % slab.ix_lim);
+    const long long rr = g / slab.ix_lim;
+    const int jj = (int)(rr % slab.iy_lim);
+    const int kz = (int)(rr / slab.iy_lim);
+    P = i + (long long)slab.nx * (jj + (long long)slab.ny * kz);
+  }
+  const bool mem1 = J0 + l < k;  // member J0 + l exists (member l always does: k > J0)
+  const float xb0 = slab.var[P + slab.L * l];
+  const float xb1v = slab.var[P + slab.L * (mem1 ? J0 + l : l)];  // branch-free: a valid address
+  const float xb1 = mem1 ? xb1v : 0.0f;
+  // sequential fp32 sum over members 0 .. k-1 (member m: slot m / J0, lane m % J0)
+  auto seq_sum_f32 = [&](float a0, float a1) {
+    float s = 0.0f;
+    for (int mm = 0; mm < J0; ++mm) s = s + readlane_f32(a0, mm);
+    for (int mm = J0; mm < k; ++mm) s = s + readlane_f32(a1, mm - J0);
+    return s;
+  };
+  const double xb_mean = (double)(seq_sum_f32(xb0, xb1) * c.nmember_inv);  // fp32 (:671)
+  const double sk = sqrt((double)(k - 1));
+  float xa0 = (float)(xb_mean + (d + sk * y0));
+  float xa1 = mem1 ? (float)(xb_mean + (d + sk * y1)) : 0.0f;
+  if (c.use_rtpp || c.use_rtps) {
+    const float xa_mean = seq_sum_f32(xa0, xa1) * c.nmember_inv;
+    const double xp0 = (double)xb0 - xb_mean;
+    const double xp1 = mem1 ? (double)xb1 - xb_mean : 0.0;
+    float xap0 = xa0 - xa_mean;
+    float xap1 = mem1 ? xa1 - xa_mean : 0.0f;
+    if (c.use_rtpp) {
+      xap0 = (float)((double)((1.0f - c.rtpp_alpha) * xap0) + (double)c.rtpp_alpha * xp0);
+      if (mem1)
+        xap1 = (float)((double)((1.0f - c.rtpp_alpha) * xap1) + (double)c.rtpp_alpha * xp1);
+    }
+    if (c.use_rtps) {
+      double d8 = 0.0;
+      for (int mm = 0; mm < J0; ++mm) {
+        const double xp = readlane_f64(xp0, mm);
+        d8 = d8 + xp * xp;
+      }
+      for (int mm = J0; mm < k; ++mm) {
+        const double xp = readlane_f64(xp1, mm - J0);
+        d8 = d8 + xp * xp;
+      }
+      const float xb_std = (float)d8;
+      const float xa_std = seq_sum_f32(xap0 * xap0, xap1 * xap1);
+      const float f = c.rtps_alpha * sqrtf(xb_std / xa_std) - c.rtps_alpha + 1.0f;
+      xap0 = xap0 * f;
+      xap1 = xap1 * f;
+    }
+    xa0 = xa_mean + xap0;
+    xa1 = xa_mean + xap1;
+  }
+  slab.var[P + slab.L * l] = xa0;
+  if (mem1) slab.var[P + slab.L * (J0 + l)] = xa1;
+  // info.y: decade of the quadrature rule (negative when M/m exceeds the last table)
+  if (l == 0) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
+}
+
+hipError_t launch_solve_tqb_tail(hipStream_t s, int kp, SolveConsts c, SlabDev slab,
+                                 long long g0, int npts, double *ws, int2 *info) {
+  if (npts <= 0) return hipSuccess;
+  if (c.quad == nullptr || kp != kBigSplitKP || c.k <= kBigJ0 + 2) return hipErrorInvalidValue;
+  // (3 waves per SIMD, 168 VGPRs, spills 35 registers: 2.88 s per C4 variable against 2.57)
+  hipLaunchKernelGGL((solve_tqb_tail_kernel<kBigSplitKP, kBigJ0, 2>), dim3(npts), dim3(64), 0, s,
+                     c, slab, g0, npts, ws, info);
+  return hipGetLastError();
+}
+
+}  // namespace cwbl

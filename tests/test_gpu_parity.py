@@ -433,6 +433,54 @@ def test_large_ensemble_block_vs_oracle(k):
     assert rel <= INCR_TOL, rel
 
 
+@pytest.mark.parametrize("k,sparse", [(97, False), (101, True), (127, False), (128, False),
+                                      (128, True)])
+def test_split_kp128_path_vs_one_kernel_and_oracle(k, sparse, monkeypatch):
+    """The KP = 128 slab path runs split by default: solve_tq_big_kernel<128, false, 64>
+    (256 threads per point) hands the trailing 64x64 matrix and its 64 reflectors to
+    solve_tqb_tail_kernel (one point per wavefront).  k < 128 exercises the identity padding;
+    the sparse obs set gives points with p < k (rank-deficient Yb Yb^T, exactly-zero
+    reflectors, tau = 0).  Against the one-kernel path (CWBL_BIG_SPLIT=0) on the whole
+    30x30x50 grid and the oracle on a 5x5-column block; hand-off batches of 1024 points."""
+    import ctypes as C
+    from cwbl import synth
+    w = synth.make("c4", scale=0.1, k=k)
+    if sparse:
+        keep = np.arange(w.obs.shape[0]) % 25 == 0
+        w.obs_xyz = np.ascontiguousarray(w.obs_xyz[keep])
+        w.obs = np.ascontiguousarray(w.obs[keep])
+        w.hdxb = np.ascontiguousarray(w.hdxb[:, keep])
+    monkeypatch.setenv("CWBL_BIG_SUB", "1024")
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CWBL_BIG_SPLIT", mode)
+        _cores.clear()
+        c = abi.Core(w.k, device=0)
+        c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+        var = w.var.copy()
+        st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+        c.finalize()
+        assert np.isfinite(var).all()
+        assert st.nonconverged == 0 and st.solved > 0
+        out[mode] = (var, st.solved, st.nobs_sum)
+    _cores.clear()
+    assert out["0"][1:] == out["1"][1:]
+    if sparse:
+        assert out["1"][2] / out["1"][1] < k, out["1"][2] / out["1"][1]
+    rel = increment_rel_rms(out["1"][0], out["0"][0], w.var)
+    assert rel <= INCR_TOL, rel
+    j0, i0, nb = 12, 12, 5
+    sub = lambda a: np.ascontiguousarray(a[..., j0:j0 + nb, i0:i0 + nb])  # noqa: E731
+    ref = sub(w.var).copy()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(sub(w.x), sub(w.y), sub(w.alt), ref)),
+                                  16, C.byref(abi.Stats()))
+    assert rc == 0
+    rel = increment_rel_rms(sub(out["1"][0]), ref, sub(w.var))
+    assert rel <= INCR_TOL, rel
+
+
 def test_tune_q_matches_reference():
     """letkf_tune_q on the device (cwbl_var_params.tune_q) against the reference's compiled
     letkf_tune_q (G5): bit for bit, including the Q3 NaN columns.  The single obs lies far
