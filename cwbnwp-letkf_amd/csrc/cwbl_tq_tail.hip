@@ -78,6 +78,22 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   if (ptot == 0) return;  // no accepted observation: var unchanged (:220, :226)
   const auto *__restrict__ w = gptr(ws + (long long)gi * HO::WORDS);
 
+  // background of the point (used by the epilogue; loaded first, the latency hides behind
+  // the steps)
+  long long P = 0;
+  {
+    const long long g = g0 + gi;
+    const int i = (int)(g % slab.ix_lim);
+    const long long rr = g / slab.ix_lim;
+    const int jj = (int)(rr % slab.iy_lim);
+    const int kz = (int)(rr / slab.iy_lim);
+    P = i + (long long)slab.nx * (jj + (long long)slab.ny * kz);
+  }
+  const bool mem1 = J0 + l < k;  // member J0 + l exists (member l always does: k > J0)
+  const float xb0 = slab.var[P + slab.L * l];
+  const float xb1v = slab.var[P + slab.L * (mem1 ? J0 + l : l)];  // branch-free: a valid address
+  const float xb1 = mem1 ? xb1v : 0.0f;
+
   // ---- hand-off: trailing rows (coalesced by column), T and the vectors' prefix ----------
   double A[KT];
   sfor<KT>([&](auto cc) {
@@ -153,7 +169,7 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     const double amb = nz ? alpha - bt : 0.0;
     // A v = scal * sum_{c >= j+1} A(:, c) xt_c; x_c from lane jl, a group's eight broadcasts
     // first (16 SGPRs), then its FMAs; groups left of column j + 1 are skipped
-    double q0 = 0.0, q1 = 0.0;
+    double q[4] = {0.0, 0.0, 0.0, 0.0};  // four chains
     sfor<NG>([&](auto gg) {
       constexpr int c0 = 8 * decltype(gg)::value;
       if (c0 + 7 >= j1) {
@@ -162,12 +178,11 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         sfor<8>([&](auto ii) {
           constexpr int col = c0 + decltype(ii)::value;
           const double xt = col > j1 ? xs[ii] : col == j1 ? amb : 0.0;  // scalar selects
-          if constexpr (col % 2 == 0) q0 = fma(A[col], xt, q0);
-          else q1 = fma(A[col], xt, q1);
+          q[col % 4] = fma(A[col], xt, q[col % 4]);
         });
       }
     });
-    const double av = scal * (q0 + q1);             // (A v)_l
+    const double av = scal * ((q[0] + q[1]) + (q[2] + q[3]));  // (A v)_l
     const double s1 = tau * wave_sum_dpp(v * av);   // v^T (tau A v); v = 0 at rows <= j
     const double wl = l > jl ? fma(-0.5 * tau * s1, v, tau * av) : 0.0;
     const double wsl = wl * scal;
@@ -214,6 +229,10 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   sm.tq[J0 + l][2] = u1t;
   sm.tq[J0 + l][3] = u2t;
   __syncthreads();
+  if (c.debug_stop == 2) {  // timing ablation: stop after the tridiagonalisation
+    if (l == 0) info[gi] = make_int2(ptot, (int)(trace + u1t + u2t));
+    return;
+  }
 
   // ---- T^-1/2 u2 by quadrature, u1^T T^-1 u2 exactly (solve_tq_big_kernel's rule) --------
   // lane = node (0..31) + 32 side: side 0 walks rows 0..H-1, side 1 rows KP-1..H; node 31
@@ -286,39 +305,78 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   const int w1 = H + (KP - 1 - (J0 + l));
   double y0 = sm.Ym[l], y1 = sm.Ym[w1];
   const double d = wave_sum_dpp(fma(sm.tq[l][2], sm.Zm[l], sm.tq[J0 + l][2] * sm.Zm[w1]));
-
-  // ---- back-transform y <- Q y = H_0 H_1 ... H_{k-3} y ------------------------------------
-  for (int jl = nst - 1; jl >= 0; --jl) {  // this kernel's reflectors: the parked rows
-    const int j1 = jl + 1;
-    const double xr = parked[jl * KT + l];
-    const double vv = l == j1 ? 1.0 : (l > j1 ? sm.scl[J0 + jl] * xr : 0.0);
-    const double a = wave_sum_dpp(vv * y1);
-    y1 = fma(-sm.tau[J0 + jl] * a, vv, y1);
+  if (c.debug_stop == 3) {  // timing ablation: stop after the quadrature
+    if (l == 0) info[gi] = make_int2(ptot, (int)(d + y0 + y1));
+    return;
   }
-#pragma unroll 4
-  for (int j = J0 - 1; j >= 0; --j) {  // the hand-off's reflectors (rows > j)
-    const double h0 = w[HO::HV + j * KP + l], h1 = w[HO::HV + j * KP + J0 + l];
-    const double v0 = l > j ? h0 : 0.0;  // row j + 1 holds 1.0
-    const double a = wave_sum_dpp(fma(v0, y0, h1 * y1));
-    const double ta = sm.tau[j] * a;
-    y0 = fma(-ta, v0, y0);
-    y1 = fma(-ta, h1, y1);
+
+  // ---- back-transform y <- Q y = H_0 H_1 ... H_{k-3} y, four reflectors per reduction ------
+  // For H_a H_{a+1} H_{a+2} H_{a+3} y (H_{a+3} first): v_q . y and v_q . v_p (q < p) in one
+  // 10-value reduction, then y -= sum_q c_q v_q with c_3 = tau_3 v_3.y, c_2 = tau_2 (v_2.y -
+  // c_3 v_2.v_3), ...  Lane slots: row l (v0, y0) and row J0 + l (v1, y1).
+  auto apply4 = [&](const double (&v0)[4], const double (&v1)[4], const double (&ta)[4]) {
+    double t[12];
+    sfor<4>([&](auto qq) { t[qq] = fma(v0[qq], y0, v1[qq] * y1); });
+    constexpr int P[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
+    sfor<6>([&](auto ee) {
+      constexpr int a = P[ee][0], b = P[ee][1];
+      t[4 + ee] = fma(v0[a], v0[b], v1[a] * v1[b]);
+    });
+    t[10] = t[11] = 0.0;
+    wave_sum4_dpp(t[0], t[1], t[2], t[3]);
+    wave_sum4_dpp(t[4], t[5], t[6], t[7]);
+    wave_sum4_dpp(t[8], t[9], t[10], t[11]);
+    // t: d0..d3, G01 G02 G03 G12 G13 G23
+    const double c3 = ta[3] * t[3];
+    const double c2 = ta[2] * fma(-c3, t[9], t[2]);
+    const double c1 = ta[1] * fma(-c3, t[8], fma(-c2, t[7], t[1]));
+    const double c0 = ta[0] * fma(-c3, t[6], fma(-c2, t[5], fma(-c1, t[4], t[0])));
+    y0 = fma(-c0, v0[0], fma(-c1, v0[1], fma(-c2, v0[2], fma(-c3, v0[3], y0))));
+    y1 = fma(-c0, v1[0], fma(-c1, v1[1], fma(-c2, v1[2], fma(-c3, v1[3], y1))));
+  };
+  // the next group's reflector entries are loaded before the current group is applied
+  auto load_tail = [&](int top, double (&v1)[4], double (&ta)[4]) {
+    sfor<4>([&](auto qq) {
+      const int jl = top - 3 + qq;  // < 0: padding (H = I)
+      const int j1 = jl + 1;
+      const double xr = parked[(jl < 0 ? 0 : jl) * KT + l];
+      const double sc = sm.scl[J0 + (jl < 0 ? 0 : jl)];
+      v1[qq] = jl < 0 ? 0.0 : l == j1 ? 1.0 : (l > j1 ? sc * xr : 0.0);
+      ta[qq] = jl < 0 ? 0.0 : sm.tau[J0 + jl];
+    });
+  };
+  auto load_hand = [&](int top, double (&v0)[4], double (&v1)[4], double (&ta)[4]) {
+    sfor<4>([&](auto qq) {
+      const int j = top - 3 + qq;
+      const double h0 = w[HO::HV + j * KP + l];
+      v0[qq] = l > j ? h0 : 0.0;  // row j + 1 holds 1.0
+      v1[qq] = w[HO::HV + j * KP + J0 + l];
+      ta[qq] = sm.tau[j];
+    });
+  };
+  {
+    const double zero4[4] = {0.0, 0.0, 0.0, 0.0};
+    double v1[4], ta[4];
+    load_tail(nst - 1, v1, ta);
+    for (int top = nst - 1; top >= 0; top -= 4) {  // this kernel's reflectors: parked rows
+      double n1[4], nt[4];
+      load_tail(top - 4 >= 0 ? top - 4 : 0, n1, nt);
+      apply4(zero4, v1, ta);
+      sfor<4>([&](auto qq) { v1[qq] = n1[qq]; ta[qq] = nt[qq]; });
+    }
+  }
+  {
+    double v0[4], v1[4], ta[4];
+    load_hand(J0 - 1, v0, v1, ta);
+    for (int top = J0 - 1; top >= 0; top -= 4) {  // the hand-off's reflectors (rows > j)
+      double n0[4], n1[4], nt[4];
+      load_hand(top - 4 >= 3 ? top - 4 : 3, n0, n1, nt);
+      apply4(v0, v1, ta);
+      sfor<4>([&](auto qq) { v0[qq] = n0[qq]; v1[qq] = n1[qq]; ta[qq] = nt[qq]; });
+    }
   }
 
   // ---- analysis and RTPP / RTPS (:671-698), fp32 in the reference's order -----------------
-  long long P = 0;
-  {
-    const long long g = g0 + gi;
-    const int i = (int)(g % slab.ix_lim);
-    const long long rr = g / slab.ix_lim;
-    const int jj = (int)(rr % slab.iy_lim);
-    const int kz = (int)(rr / slab.iy_lim);
-    P = i + (long long)slab.nx * (jj + (long long)slab.ny * kz);
-  }
-  const bool mem1 = J0 + l < k;  // member J0 + l exists (member l always does: k > J0)
-  const float xb0 = slab.var[P + slab.L * l];
-  const float xb1v = slab.var[P + slab.L * (mem1 ? J0 + l : l)];  // branch-free: a valid address
-  const float xb1 = mem1 ? xb1v : 0.0f;
   // sequential fp32 sum over members 0 .. k-1 (member m: slot m / J0, lane m % J0)
   auto seq_sum_f32 = [&](float a0, float a1) {
     float s = 0.0f;
