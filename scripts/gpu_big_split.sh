@@ -11,7 +11,7 @@ for sp in ${SPLITS:-1 0}; do
   echo -n "split=$sp: "; tail -1 gpurun_out/bench_c4_$sp.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('value %.4g ms/step %.1f solve %.1f search %.1f TF %.2f' % (d['value'], d['ms_per_step'], d['detail']['ms_solve_per_step'], d['detail']['ms_search_per_step'], d['roofline']['achieved']))"
 done
 if [ -n "$PROF" ]; then
-  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_c4 -o c4 -- python3 $GRAFT_REPO_ROOT/bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline --no-cycle > $GRAFT_REPO_ROOT/gpurun_out/prof_c4.log 2>&1
+  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_c4 -o c4 --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline --no-cycle > $GRAFT_REPO_ROOT/gpurun_out/prof_c4.log 2>&1
   echo "prof rc=$?"; cd $GRAFT_REPO_ROOT
   f=$(find gpurun_out/prof_c4 -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cut -d, -f1-8 "$f" | head -8
 fi
