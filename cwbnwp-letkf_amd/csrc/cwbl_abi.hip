@@ -81,10 +81,12 @@ struct TreeBufs {
   int entry = -1, dim = 0, depth = 0;
   float hinv = 0.0f, vinv = 0.0f;
   DevBuf nodes, rdata, ind, col_bg, col_omm, col_err, col_ok;
+  DevBuf bxyz, bstart;  // uniform bins of the same coordinates (search_binned_kernel)
   HostTree host;
+  HostBins bins;
   void release() {
     nodes.release(); rdata.release(); ind.release(); col_bg.release();
-    col_omm.release(); col_err.release(); col_ok.release();
+    col_omm.release(); col_err.release(); col_ok.release(); bxyz.release(); bstart.release();
   }
 };
 
@@ -113,6 +115,8 @@ struct State {
   DevBuf qxyz, qnf, qidx, qr2;                        // search staging
   DevBuf quad;                                        // x^-1/2 quadrature tables
   DevBuf wsa;                                         // hand-off records (split KP=40 path)
+  DevBuf flags;                                       // binned search: flagged points (+ count)
+  bool binned = true;                                 // CWBL_SEARCH=tree: k-d tree search only
   bool jacobi = false;                                // CWBL_SOLVER=jacobi: eigen path
   bool tq4 = true;                                    // CWBL_TQ4=0: one-kernel KP=40 solve
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: hand-off batch (points)
@@ -249,6 +253,15 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
       if (!h.ind.empty())
         HIPCHK(hipMemcpyAsync(nt->ind.p, h.ind.data(), h.ind.size() * sizeof(int),
                               hipMemcpyHostToDevice, S.stream));
+      build_bins(h, tdim, std::sqrt(search_r2()), nt->bins);
+      const HostBins &hb = nt->bins;
+      HIPCHK(nt->bxyz.ensure(hb.xyzs.size() * sizeof(float) + 16));
+      HIPCHK(nt->bstart.ensure(hb.start.size() * sizeof(int)));
+      if (!hb.xyzs.empty())
+        HIPCHK(hipMemcpyAsync(nt->bxyz.p, hb.xyzs.data(), hb.xyzs.size() * sizeof(float),
+                              hipMemcpyHostToDevice, S.stream));
+      HIPCHK(hipMemcpyAsync(nt->bstart.p, hb.start.data(), hb.start.size() * sizeof(int),
+                            hipMemcpyHostToDevice, S.stream));
       tb = nt.get();
       S.tree_cache.push_back(std::move(nt));
     }
@@ -286,6 +299,10 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
     d.max_lz = tp->max_lz_pts;
     d.list_off = list_cap;
     d.q1_undef = q1u;
+    d.bxyz = tb->bxyz.as<float4>();
+    d.bstart = tb->bstart.as<int>();
+    d.bx0 = tb->bins.x0; d.by0 = tb->bins.y0; d.bz0 = tb->bins.z0; d.binv = tb->bins.binv;
+    d.nbx = tb->bins.nbx; d.nby = tb->bins.nby; d.nbz = tb->bins.nbz;
     list_cap += list_span(tp->max_lz_pts);
     max_depth = std::max(max_depth, tb->depth);
     descs.push_back(d);
@@ -307,7 +324,7 @@ void release_all() {
   release_obs();
   for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.nbr_cnt2, &S.nbr_idx2, &S.info, &S.stats, &S.sx,
                     &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev,
-                    &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad, &S.wsa})
+                    &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad, &S.wsa, &S.flags})
     b->release();
   for (hipEvent_t e : S.events) (void)hipEventDestroy(e);
   S.events.clear();
@@ -394,6 +411,10 @@ int cwbl_init(const cwbl_init_params *p) {
   if (const char *e = std::getenv("CWBL_TQ4_SUB")) S.tq4_sub = std::atoll(e);
   S.big_split = true;
   S.big_sub = 32768;
+  {
+    const char *e = std::getenv("CWBL_SEARCH");
+    S.binned = !(e && std::strcmp(e, "tree") == 0);
+  }
   if (const char *e = std::getenv("CWBL_BIG_SPLIT")) S.big_split = std::atoi(e) != 0;
   if (const char *e = std::getenv("CWBL_BIG_SUB")) S.big_sub = std::max(64LL, std::atoll(e));
   if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
@@ -571,6 +592,10 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     HIPCHK(S.nbr_idx2.ensure(bytes_idx));
   }
   HIPCHK(S.info.ensure((size_t)B * sizeof(int2)));
+  HIPCHK(S.flags.ensure((size_t)(B + 1) * sizeof(int)));
+  // bounding-box half-width of the binned search: the radius with a margin, so that every
+  // point with d2 <= r2 in fp32 lies inside
+  const float rbox = std::sqrt(search_r2()) * 1.0001f + 1e-5f;
   HIPCHK(S.stats.ensure(sizeof(DevStats)));
   HIPCHK(hipMemsetAsync(S.stats.p, 0, sizeof(DevStats), S.stream));
   SolveConsts c = solve_consts((float)(S.k - 1) / vp->multi_infl,  // inflat (:68)
@@ -603,8 +628,17 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     hipStream_t ss = S.serial_search ? S.stream : S.sstream;
     if (bi >= 2) HIPCHK(hipStreamWaitEvent(ss, S.events[done_ev[bi - 2]], 0));
     HIPCHK(hipEventRecord(a, ss));
-    HIPCHK(launch_search(ss, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb, ncnt,
-                         nidx, nullptr, dst));
+    if (S.binned) {  // bins; the tree search redoes the points whose lists pass max_lz
+      int *fcnt = S.flags.as<int>(), *fidx = fcnt + 1;
+      HIPCHK(hipMemsetAsync(fcnt, 0, sizeof(int), ss));
+      HIPCHK(launch_search_binned(ss, dtrees, nt, list_cap, c.r2, rbox, sd, g0, nb, ncnt, nidx,
+                                  fcnt, fidx));
+      HIPCHK(launch_search_flagged(ss, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb, fcnt,
+                                   fidx, ncnt, nidx, dst));
+    } else {
+      HIPCHK(launch_search(ss, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb, ncnt,
+                           nidx, nullptr, dst));
+    }
     HIPCHK(hipEventRecord(b, ss));
     HIPCHK(hipStreamWaitEvent(S.stream, b, 0));
     HIPCHK(hipEventRecord(b2, S.stream));

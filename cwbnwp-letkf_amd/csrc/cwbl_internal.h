@@ -53,7 +53,26 @@ struct TreeDesc {
   int   max_lz;
   int   list_off;             // offset of this type inside a point's neighbour list
   int   q1_undef;
+  // uniform bins over the same normalised coordinates (search_binned_kernel): cell
+  // (ix, iy, iz) = floor((x - b0) * binv) per dimension, cells x-fastest; bxyz holds the
+  // points cell by cell (tree-slot order within a cell) with the slot in .w (int bits),
+  // bstart[c] .. bstart[c + 1] the points of cell c
+  const float4 *bxyz;
+  const int    *bstart;
+  float bx0, by0, bz0, binv;
+  int   nbx, nby, nbz;
 };
+
+// Host-side bins of one tree (build_bins, kdtree_build.cpp).
+struct HostBins {
+  float x0 = 0.0f, y0 = 0.0f, z0 = 0.0f, binv = 1.0f;
+  int nbx = 1, nby = 1, nbz = 1;
+  std::vector<float> xyzs;   // 4 floats per point: x, y, z, slot (int bits)
+  std::vector<int> start;    // ncells + 1
+};
+// Bins of side ~r/2 (r: the search radius in normalised units) over a built tree's
+// rearranged coordinates; dim 2 ignores z.  Capped at 2^22 cells.
+void build_bins(const HostTree &t, int dim, float r, HostBins &out);
 
 // Per-variable constants of the solve.
 struct SolveConsts {
@@ -206,6 +225,20 @@ hipError_t launch_solve_tq_big(hipStream_t s, int kp, bool assembled, const Tree
                                const int *nbr_cnt, const int *nbr_idx,
                                const long long *col_off, const float *yo, const float *yb,
                                const float *xb, float *xa, int2 *info);
+
+// The analysis search from uniform bins: the same fixed-radius sets as launch_search (the
+// same fp32 distances and <= r2 test) in bin order, which differs from kdtree2's visiting
+// order; a point whose list would pass max_lz on any tree is appended to flag_idx
+// (flag_cnt, zeroed by the caller) for launch_search_flagged, which reruns the tree search
+// there so Q4 truncation keeps the reference's order.  rbox: the bounding-box half-width,
+// sqrt(r2) with a margin.
+hipError_t launch_search_binned(hipStream_t s, const TreeDesc *trees, int ntrees, int list_cap,
+                                float r2, float rbox, SlabDev slab, long long g0, int npts,
+                                int *nbr_cnt, int *nbr_idx, int *flag_cnt, int *flag_idx);
+hipError_t launch_search_flagged(hipStream_t s, const TreeDesc *trees, int ntrees, int depth,
+                                 int list_cap, float r2, SlabDev slab, long long g0, int npts,
+                                 const int *flag_cnt, const int *flag_idx, int *nbr_cnt,
+                                 int *nbr_idx, DevStats *stats);
 
 hipError_t launch_search_single(hipStream_t s, const TreeDesc *tree, int depth, float r2,
                                 int nq, const float *q_xyz, int max_lz, int *nfound, int *idx,

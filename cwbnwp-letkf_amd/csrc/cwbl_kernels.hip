@@ -215,6 +215,11 @@ __device__ int search_tree(const TreeDesc &T, float q0, float q1, float q2, floa
 struct SlabQuery {
   SlabDev s;
   long long g0;
+  // thread li -> batch point gi (false: no point)
+  __device__ bool map(int li, int npts, int &gi) const {
+    gi = li;
+    return li < npts;
+  }
   __device__ void at(int gi, float &x, float &y, float &z) const {
     const long long g = g0 + gi;
     const int i = (int)(g % s.ix_lim);
@@ -229,11 +234,27 @@ struct SlabQuery {
 
 struct ListQuery {
   const float *q;  // (3,nq)
+  __device__ bool map(int li, int npts, int &gi) const {
+    gi = li;
+    return li < npts;
+  }
   __device__ void at(int gi, float &x, float &y, float &z) const {
     x = q[3 * (long long)gi];
     y = q[3 * (long long)gi + 1];
     z = q[3 * (long long)gi + 2];
   }
+};
+
+// the batch points the binned search flagged (their lists would pass max_lz)
+struct FlagQuery {
+  SlabQuery sq;
+  const int *cnt, *idx;
+  __device__ bool map(int li, int, int &gi) const {
+    if (li >= *cnt) return false;
+    gi = idx[li];
+    return true;
+  }
+  __device__ void at(int gi, float &x, float &y, float &z) const { sq.at(gi, x, y, z); }
 };
 
 template <class Q>
@@ -244,8 +265,8 @@ search_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, floa
   // traversal stacks, one column per lane; sized by the host to the deepest tree, so a
   // shallow tree leaves LDS for more resident waves (the search is latency bound)
   extern __shared__ int stk[];
-  const int gi = blockIdx.x * 64 + threadIdx.x;
-  if (gi >= npts) return;
+  int gi;
+  if (!qs.map(blockIdx.x * 64 + threadIdx.x, npts, gi)) return;
   float px, py, pz;
   qs.at(gi, px, py, pz);
   unsigned trunc = 0;
@@ -281,6 +302,134 @@ hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int d
   hipLaunchKernelGGL(search_kernel<SlabQuery>, dim3((npts + 63) / 64), dim3(64),
                      stack_bytes(depth), s, trees,
                      ntrees, list_cap, r2, q, npts, nbr_cnt, nbr_idx, nbr_r2, stats);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// search_binned_kernel: one lane per grid point.  The fixed-radius sets of search_kernel
+// (same normalisation, the same fp32 distance d - q in dimension order and d2 <= r2 test as
+// process_terminal_node_fixedball, module_kdtree2.f90:1654-1707) from uniform bins: the
+// cells of the ball's bounding box are, per (iy, iz), one contiguous run of points, so a
+// lane streams through at most 5 x 5 runs instead of walking the tree (divergent, latency
+// bound).  The sets are identical; the order is the bins', which only changes the order of
+// the fp64 sums of the solve.  Where kdtree2's order decides WHICH points are kept (a list
+// past max_lz, Q4) the point is flagged and search_kernel<FlagQuery> redoes it.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64)
+search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, float r2,
+                     float rbox, SlabQuery qs, int npts, int *__restrict__ nbr_cnt,
+                     int *__restrict__ nbr_idx, int *__restrict__ flag_cnt,
+                     int *__restrict__ flag_idx) {
+  const int gi = blockIdx.x * 64 + threadIdx.x;
+  if (gi >= npts) return;
+  float px, py, pz;
+  qs.at(gi, px, py, pz);
+  bool flagged = false;
+  for (int t = 0; t < ntrees; ++t) {
+    const TreeDesc &T = trees[t];
+    const float q0 = px * T.hclr_inv, q1 = py * T.hclr_inv;  // get_lz (:243-253)
+    const float q2 = T.query3d ? pz * T.vclr_inv : 0.0f;
+    int *__restrict__ out = nbr_idx + list_index(gi, list_cap, T.list_off);
+    const int dim = T.tree_dim, max_lz = T.max_lz;
+    int count = 0;
+    bool ovf = false;
+    int4 grp = make_int4(0, 0, 0, 0);
+    if (max_lz > 0) {
+      // conservative cell range of [q - rbox, q + rbox] (clamped before the int conversion)
+      auto crange = [&](float q, float b0, int nb, int &a, int &b) {
+        const float lo = (q - rbox - b0) * T.binv, hi = (q + rbox - b0) * T.binv;
+        a = (int)fminf(fmaxf(floorf(lo), 0.0f), (float)nb);
+        b = (int)fminf(fmaxf(floorf(hi), -1.0f), (float)(nb - 1));
+      };
+      int ix0, ix1, iy0, iy1, iz0 = 0, iz1 = 0;
+      crange(q0, T.bx0, T.nbx, ix0, ix1);
+      crange(q1, T.by0, T.nby, iy0, iy1);
+      if (dim == 3) crange(q2, T.bz0, T.nbz, iz0, iz1);
+      if (ix0 > ix1) iy1 = iy0 - 1;  // the box misses the grid in x
+      // distance from q to the slab of cell row/layer i along one axis, shrunk by a margin
+      // (conservative against the fp32 cell assignment)
+      const float h = 1.0f / T.binv, rb2 = rbox * rbox;
+      auto gap = [&](float q, float b0, int i) {
+        const float lo = b0 + (float)i * h, hi = lo + h;
+        const float g = fmaxf(fmaxf(lo - q, q - hi), 0.0f);
+        return fmaxf(g - 1e-3f * h, 0.0f);
+      };
+      for (int iz = iz0; iz <= iz1 && !ovf; ++iz) {
+        const float gz = dim == 3 ? gap(q2, T.bz0, iz) : 0.0f;
+        for (int iy = iy0; iy <= iy1 && !ovf; ++iy) {
+          // the ball's x-extent over this row of cells
+          const float gy = gap(q1, T.by0, iy);
+          const float rem = rb2 - gy * gy - gz * gz;
+          if (rem < 0.0f) continue;
+          const float xh = sqrtf(rem);
+          const int jx0 = max(ix0, (int)fminf(fmaxf(floorf((q0 - xh - T.bx0) * T.binv), 0.0f),
+                                               (float)T.nbx));
+          const int jx1 = min(ix1, (int)fminf(fmaxf(floorf((q0 + xh - T.bx0) * T.binv), -1.0f),
+                                               (float)(T.nbx - 1)));
+          if (jx0 > jx1) continue;
+          const int cb = (iz * T.nby + iy) * T.nbx;
+          const int e = T.bstart[cb + jx1 + 1];
+          for (int i0 = T.bstart[cb + jx0]; i0 < e; i0 += kAhead) {
+            float4 d[kAhead];
+#pragma unroll
+            for (int a = 0; a < kAhead; ++a) d[a] = T.bxyz[min(i0 + a, e - 1)];
+#pragma unroll
+            for (int a = 0; a < kAhead; ++a) {
+              const float dx = d[a].x - q0, dy = d[a].y - q1;
+              float sd = dx * dx;
+              sd = sd + dy * dy;
+              if (dim == 3) {
+                const float dz = d[a].z - q2;
+                sd = sd + dz * dz;
+              }
+              if (i0 + a < e && sd <= r2 && !ovf) {
+                if (count == max_lz) {
+                  ovf = true;
+                } else {
+                  const int slot = __float_as_int(d[a].w);
+                  const int g = count % kListGroup;
+                  grp.x = g == 0 ? slot : grp.x;
+                  grp.y = g == 1 ? slot : grp.y;
+                  grp.z = g == 2 ? slot : grp.z;
+                  grp.w = slot;
+                  if (g == kListGroup - 1)
+                    *reinterpret_cast<int4 *>(out + list_slot(count - g)) = grp;
+                  ++count;
+                }
+              }
+            }
+            if (ovf) break;
+          }
+        }
+      }
+      if (count % kListGroup != 0)
+        *reinterpret_cast<int4 *>(out + list_slot(count - count % kListGroup)) = grp;
+    }
+    nbr_cnt[(long long)gi * ntrees + t] = count;
+    flagged = flagged || ovf;
+  }
+  if (flagged) flag_idx[atomicAdd(flag_cnt, 1)] = gi;
+}
+
+hipError_t launch_search_binned(hipStream_t s, const TreeDesc *trees, int ntrees, int list_cap,
+                                float r2, float rbox, SlabDev slab, long long g0, int npts,
+                                int *nbr_cnt, int *nbr_idx, int *flag_cnt, int *flag_idx) {
+  if (npts <= 0) return hipSuccess;
+  SlabQuery q{slab, g0};
+  hipLaunchKernelGGL(search_binned_kernel, dim3((npts + 63) / 64), dim3(64), 0, s, trees,
+                     ntrees, list_cap, r2, rbox, q, npts, nbr_cnt, nbr_idx, flag_cnt, flag_idx);
+  return hipGetLastError();
+}
+
+hipError_t launch_search_flagged(hipStream_t s, const TreeDesc *trees, int ntrees, int depth,
+                                 int list_cap, float r2, SlabDev slab, long long g0, int npts,
+                                 const int *flag_cnt, const int *flag_idx, int *nbr_cnt,
+                                 int *nbr_idx, DevStats *stats) {
+  if (npts <= 0) return hipSuccess;
+  FlagQuery q{SlabQuery{slab, g0}, flag_cnt, flag_idx};
+  hipLaunchKernelGGL(search_kernel<FlagQuery>, dim3((npts + 63) / 64), dim3(64),
+                     stack_bytes(depth), s, trees, ntrees, list_cap, r2, q, npts, nbr_cnt,
+                     nbr_idx, (float *)nullptr, stats);
   return hipGetLastError();
 }
 

@@ -12,6 +12,8 @@
 #include "cwbl_internal.h"
 
 #include <algorithm>
+#include <cmath>
+#include <cstring>
 
 namespace cwbl {
 namespace {
@@ -114,6 +116,53 @@ void build_kdtree(const float *xyz3, int n, int dim, HostTree &out) {
   for (int i = 0; i < n; ++i)
     for (int d = 0; d < 3; ++d)
       out.rdata[4 * static_cast<size_t>(i) + d] = d < dim ? xyz3[3 * out.ind[i] + d] : 0.0f;
+}
+
+void build_bins(const HostTree &t, int dim, float r, HostBins &out) {
+  const int n = t.n;
+  out = HostBins{};
+  float lo[3] = {0.0f, 0.0f, 0.0f}, hi[3] = {0.0f, 0.0f, 0.0f};
+  for (int i = 0; i < n; ++i)
+    for (int c = 0; c < 3; ++c) {
+      const float v = t.rdata[4 * (size_t)i + c];
+      lo[c] = i == 0 ? v : std::min(lo[c], v);
+      hi[c] = i == 0 ? v : std::max(hi[c], v);
+    }
+  if (dim < 3) lo[2] = hi[2] = 0.0f;
+  float h = 0.5f * r;
+  long long nb[3];
+  for (;;) {
+    for (int c = 0; c < 3; ++c)
+      nb[c] = std::max(1LL, (long long)std::floor((double)(hi[c] - lo[c]) / h) + 1);
+    if (nb[0] * nb[1] * nb[2] <= (1LL << 22)) break;
+    h *= 1.25f;
+  }
+  out.x0 = lo[0]; out.y0 = lo[1]; out.z0 = lo[2];
+  out.binv = 1.0f / h;
+  out.nbx = (int)nb[0]; out.nby = (int)nb[1]; out.nbz = (int)nb[2];
+  // the kernel's cell arithmetic, in fp32 (monotone, so the query's conservative box
+  // brackets every cell a point within r can fall in)
+  auto cell = [&](int c, float v) {
+    const float f = (v - (c == 0 ? out.x0 : c == 1 ? out.y0 : out.z0)) * out.binv;
+    return (long long)std::min<float>(std::max(std::floor(f), 0.0f), (float)(nb[c] - 1));
+  };
+  const long long ncell = nb[0] * nb[1] * nb[2];
+  std::vector<long long> cid(n);
+  out.start.assign(ncell + 1, 0);
+  for (int i = 0; i < n; ++i) {
+    const float *d = &t.rdata[4 * (size_t)i];
+    const long long cz = dim == 3 ? cell(2, d[2]) : 0;
+    cid[i] = cell(0, d[0]) + nb[0] * (cell(1, d[1]) + nb[1] * cz);
+    ++out.start[cid[i] + 1];
+  }
+  for (long long c = 0; c < ncell; ++c) out.start[c + 1] += out.start[c];
+  std::vector<int> fill(out.start.begin(), out.start.end() - 1);
+  out.xyzs.assign(4 * (size_t)n, 0.0f);
+  for (int i = 0; i < n; ++i) {  // slot order within a cell
+    const int p = fill[cid[i]]++;
+    std::memcpy(&out.xyzs[4 * (size_t)p], &t.rdata[4 * (size_t)i], 3 * sizeof(float));
+    std::memcpy(&out.xyzs[4 * (size_t)p + 3], &i, sizeof(int));
+  }
 }
 
 }  // namespace cwbl

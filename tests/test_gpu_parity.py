@@ -550,3 +550,46 @@ def test_large_k_random_batch_vs_oracle(k):
                               inflat, 1, 0.7, 1, 0.3, want_evals=False)
         rel = increment_rel_rms(xa[i], ref, xb[i])
         assert rel <= INCR_TOL, (p, rel)
+
+
+@pytest.mark.parametrize("name", ["c2", "c5", "driver_mixed.npz", "driver_c1.npz"])
+def test_binned_search_equals_tree_search(name, monkeypatch):
+    """The analysis search runs on uniform bins (search_binned_kernel) with the k-d tree as
+    the fallback where max_lz truncates (Q4).  The neighbour SETS are identical, so the solved
+    points, the accepted-obs counts and the truncation counts must match the tree search's
+    exactly; the column order differs, which moves only the fp64 sums (increments to ~1e-12).
+    driver_mixed has truncated lists (tree fallback), C5-shaped dense radar has ~1300
+    neighbours per point."""
+    from cwbl import synth
+    if name.endswith(".npz"):
+        case = DriverCase(name)
+        mk = lambda: (abi.Core(case.k, device=0, weight_function=case.wf,  # noqa: E731
+                               norain_value=case.norain), case.obs_set(), case.vp)
+        slabs = lambda: case.slab()  # noqa: E731
+        var_in = case.var_in
+    else:
+        w = synth.make(name, scale=0.12 if name == "c2" else 0.04)
+        ob = lambda: abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs,  # noqa: E731
+                                                    w.hdxb).build()
+        mk = lambda: (abi.Core(w.k, device=0), ob(), w.vp)  # noqa: E731
+
+        def slabs():
+            var = w.var.copy()
+            return abi.make_slab(w.x, w.y, w.alt, var), var
+        var_in = w.var
+    out = {}
+    for mode in ("tree", "bins"):
+        monkeypatch.setenv("CWBL_SEARCH", mode)
+        _cores.clear()
+        c, obs, vp = mk()
+        c.set_obs(obs)
+        slab, var = slabs()
+        st = c.analyze_var(vp, slab)
+        c.finalize()
+        out[mode] = (var, st.solved, st.nobs_sum, st.lz_truncated, st.max_p)
+    _cores.clear()
+    assert out["tree"][1:] == out["bins"][1:], (out["tree"][1:], out["bins"][1:])
+    if name == "driver_mixed.npz":
+        assert out["bins"][3] > 0  # the fallback ran
+    rel = increment_rel_rms(out["bins"][0], out["tree"][0], var_in)
+    assert rel <= 1e-9, rel
