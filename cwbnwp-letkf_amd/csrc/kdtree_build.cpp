@@ -121,19 +121,24 @@ void build_kdtree(const float *xyz3, int n, int dim, HostTree &out) {
 void build_bins(const HostTree &t, int dim, float r, HostBins &out) {
   const int n = t.n;
   out = HostBins{};
+  // bounds over the finite coordinates (a non-finite point is never within r: d2 <= r2 fails
+  // for NaN or inf, so it may sit in any cell; it goes to cell 0)
   float lo[3] = {0.0f, 0.0f, 0.0f}, hi[3] = {0.0f, 0.0f, 0.0f};
+  bool seen[3] = {false, false, false};
   for (int i = 0; i < n; ++i)
     for (int c = 0; c < 3; ++c) {
       const float v = t.rdata[4 * (size_t)i + c];
-      lo[c] = i == 0 ? v : std::min(lo[c], v);
-      hi[c] = i == 0 ? v : std::max(hi[c], v);
+      if (!std::isfinite(v)) continue;
+      lo[c] = seen[c] ? std::min(lo[c], v) : v;
+      hi[c] = seen[c] ? std::max(hi[c], v) : v;
+      seen[c] = true;
     }
   if (dim < 3) lo[2] = hi[2] = 0.0f;
   float h = 0.5f * r;
   long long nb[3];
   for (;;) {
     for (int c = 0; c < 3; ++c)
-      nb[c] = std::max(1LL, (long long)std::floor((double)(hi[c] - lo[c]) / h) + 1);
+      nb[c] = 1 + (long long)std::min(std::floor(((double)hi[c] - (double)lo[c]) / h), 4194304.0);
     if (nb[0] * nb[1] * nb[2] <= (1LL << 22)) break;
     h *= 1.25f;
   }
@@ -144,6 +149,7 @@ void build_bins(const HostTree &t, int dim, float r, HostBins &out) {
   // brackets every cell a point within r can fall in)
   auto cell = [&](int c, float v) {
     const float f = (v - (c == 0 ? out.x0 : c == 1 ? out.y0 : out.z0)) * out.binv;
+    if (!std::isfinite(f)) return 0LL;
     return (long long)std::min<float>(std::max(std::floor(f), 0.0f), (float)(nb[c] - 1));
   };
   const long long ncell = nb[0] * nb[1] * nb[2];
@@ -151,8 +157,9 @@ void build_bins(const HostTree &t, int dim, float r, HostBins &out) {
   out.start.assign(ncell + 1, 0);
   for (int i = 0; i < n; ++i) {
     const float *d = &t.rdata[4 * (size_t)i];
+    const bool fin = std::isfinite(d[0]) && std::isfinite(d[1]) && (dim < 3 || std::isfinite(d[2]));
     const long long cz = dim == 3 ? cell(2, d[2]) : 0;
-    cid[i] = cell(0, d[0]) + nb[0] * (cell(1, d[1]) + nb[1] * cz);
+    cid[i] = fin ? cell(0, d[0]) + nb[0] * (cell(1, d[1]) + nb[1] * cz) : 0;
     ++out.start[cid[i] + 1];
   }
   for (long long c = 0; c < ncell; ++c) out.start[c + 1] += out.start[c];
