@@ -331,7 +331,10 @@ def main():
         achieved = flops / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else 0.0
         kp = ((k + 7) // 8) * 8 if k <= 64 else (96 if k <= 96 else 128)
         split = (not jacobi and kp == 40 and os.environ.get("CWBL_TQ4", "1") != "0")
+        split128 = kp == 128 and k > 66 and os.environ.get("CWBL_BIG_SPLIT", "1") != "0"
         kname = ("solve_tq_kernel<40, false, 8> + solve_tq4_kernel<40, 8>" if split else
+                 "solve_tq_big_kernel<128, false, 64> + solve_tqb_tail_kernel<128, 64, 2>"
+                 if split128 else
                  ("solve_kernel" if jacobi else
                   "solve_tq_kernel" if kp <= 64 else "solve_tq_big_kernel") + f"<{kp}, false>")
         traffic = None  # HBM bytes per launch from the committed PMC pass of this kernel
