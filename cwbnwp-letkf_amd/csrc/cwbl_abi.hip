@@ -642,13 +642,15 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     HIPCHK(hipEventRecord(b, ss));
     HIPCHK(hipStreamWaitEvent(S.stream, b, 0));
     HIPCHK(hipEventRecord(b2, S.stream));
-    if (S.kp == kBigSplitKP && S.big_split && S.k > kBigJ0 + 2) {
+    if ((S.kp == 96 || S.kp == kBigSplitKP) && S.big_split && S.k > big_split_j0(S.kp) + 2) {
       // 256-thread assembly + first kBigJ0 steps -> workspace -> one-wavefront tail, in
       // hand-off batches of Bs points (a multiple of kListLanes; ~100 KB per point)
       const long long nsub = (nb + S.big_sub - 1) / S.big_sub;
       long long Bs = (nb + nsub - 1) / nsub;
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
-      HIPCHK(S.wsa.ensure((size_t)Bs * BigHandoff<kBigSplitKP, kBigJ0>::WORDS * 8));
+      HIPCHK(S.wsa.ensure((size_t)Bs * 8 *
+                          (S.kp == 96 ? BigHandoff<96, 32>::WORDS
+                                      : BigHandoff<kBigSplitKP, kBigJ0>::WORDS)));
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
         const int ns = (int)std::min<long long>(Bs, nb - s0);
         HIPCHK(launch_big_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,

@@ -197,8 +197,10 @@ hipError_t launch_solve_tq4(hipStream_t s, int kp, SolveConsts c, SlabDev slab, 
 // (KP-J0)^2 matrix, its J0 reflectors, T so far and Q^T b1, Q^T x' over through the
 // workspace (BigHandoff, info[gi] = (p, 0)); solve_tqb_tail_kernel (cwbl_tq_tail.hip)
 // finishes with one point per wavefront, lane l holding the full trailing row J0 + l.
+// (KP = 96, k = 65..96: the same with the hand-off after 32 steps)
 constexpr int kBigSplitKP = 128;
 constexpr int kBigJ0 = 64;
+constexpr int big_split_j0(int kp) { return kp - 64; }
 // fp64 words of one point's hand-off record
 template <int KP, int J0>
 struct BigHandoff {

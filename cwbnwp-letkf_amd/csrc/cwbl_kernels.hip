@@ -315,6 +315,7 @@ hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int d
 // the fp64 sums of the solve.  Where kdtree2's order decides WHICH points are kept (a list
 // past max_lz, Q4) the point is flagged and search_kernel<FlagQuery> redoes it.
 // ---------------------------------------------------------------------------------------
+constexpr int kBinAhead = 8;  // bin points loaded ahead of their tests
 __global__ void __launch_bounds__(64)
 search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, float r2,
                      float rbox, SlabQuery qs, int npts, int *__restrict__ nbr_cnt,
@@ -336,8 +337,12 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
     int4 grp = make_int4(0, 0, 0, 0);
     if (max_lz > 0) {
       // conservative cell range of [q - rbox, q + rbox] (clamped before the int conversion)
+      // (the margin also covers the rounding of q -/+ rbox and of the cell arithmetic, which
+      // grows with the coordinates' magnitude)
+      auto margin = [&](float q, float b0) { return 2e-6f * (fabsf(q) + fabsf(b0)); };
       auto crange = [&](float q, float b0, int nb, int &a, int &b) {
-        const float lo = (q - rbox - b0) * T.binv, hi = (q + rbox - b0) * T.binv;
+        const float rq = rbox + margin(q, b0);
+        const float lo = (q - rq - b0) * T.binv, hi = (q + rq - b0) * T.binv;
         a = (int)fminf(fmaxf(floorf(lo), 0.0f), (float)nb);
         b = (int)fminf(fmaxf(floorf(hi), -1.0f), (float)(nb - 1));
       };
@@ -352,7 +357,7 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
       auto gap = [&](float q, float b0, int i) {
         const float lo = b0 + (float)i * h, hi = lo + h;
         const float g = fmaxf(fmaxf(lo - q, q - hi), 0.0f);
-        return fmaxf(g - 1e-3f * h, 0.0f);
+        return fmaxf(g - 1e-3f * h - margin(q, b0), 0.0f);
       };
       for (int iz = iz0; iz <= iz1 && !ovf; ++iz) {
         const float gz = dim == 3 ? gap(q2, T.bz0, iz) : 0.0f;
@@ -361,7 +366,7 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
           const float gy = gap(q1, T.by0, iy);
           const float rem = rb2 - gy * gy - gz * gz;
           if (rem < 0.0f) continue;
-          const float xh = sqrtf(rem);
+          const float xh = sqrtf(rem) + margin(q0, T.bx0);
           const int jx0 = max(ix0, (int)fminf(fmaxf(floorf((q0 - xh - T.bx0) * T.binv), 0.0f),
                                                (float)T.nbx));
           const int jx1 = min(ix1, (int)fminf(fmaxf(floorf((q0 + xh - T.bx0) * T.binv), -1.0f),
@@ -369,12 +374,12 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
           if (jx0 > jx1) continue;
           const int cb = (iz * T.nby + iy) * T.nbx;
           const int e = T.bstart[cb + jx1 + 1];
-          for (int i0 = T.bstart[cb + jx0]; i0 < e; i0 += kAhead) {
-            float4 d[kAhead];
+          for (int i0 = T.bstart[cb + jx0]; i0 < e; i0 += kBinAhead) {
+            float4 d[kBinAhead];
 #pragma unroll
-            for (int a = 0; a < kAhead; ++a) d[a] = T.bxyz[min(i0 + a, e - 1)];
+            for (int a = 0; a < kBinAhead; ++a) d[a] = T.bxyz[min(i0 + a, e - 1)];
 #pragma unroll
-            for (int a = 0; a < kAhead; ++a) {
+            for (int a = 0; a < kBinAhead; ++a) {
               const float dx = d[a].x - q0, dy = d[a].y - q1;
               float sd = dx * dx;
               sd = sd + dy * dy;

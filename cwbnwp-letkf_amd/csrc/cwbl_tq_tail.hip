@@ -66,7 +66,7 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   constexpr int KT = HO::KT;  // trailing rows: one per lane
   constexpr int H = KP / 2;   // rows walked by each side of a twisted solve
   constexpr int NG = KT / 8;  // column groups
-  static_assert(KT == 64 && J0 == 64, "one trailing row and one prefix row per lane");
+  static_assert(KT == 64 && J0 <= 64 && J0 % 4 == 0, "one trailing row per lane; prefix rows on lanes < J0");
   using SM = TailSmem<KP, J0>;
   __shared__ SM sm;
 
@@ -89,9 +89,11 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     const int kz = (int)(rr / slab.iy_lim);
     P = i + (long long)slab.nx * (jj + (long long)slab.ny * kz);
   }
-  const bool mem1 = J0 + l < k;  // member J0 + l exists (member l always does: k > J0)
-  const float xb0 = slab.var[P + slab.L * l];
-  const float xb1v = slab.var[P + slab.L * (mem1 ? J0 + l : l)];  // branch-free: a valid address
+  const bool mem0 = l < J0;      // prefix row / member l exists (k > J0)
+  const bool mem1 = J0 + l < k;  // member J0 + l exists
+  const float xb0v = slab.var[P + slab.L * (mem0 ? l : 0)];  // branch-free: valid addresses
+  const float xb1v = slab.var[P + slab.L * (mem1 ? J0 + l : 0)];
+  const float xb0 = mem0 ? xb0v : 0.0f;
   const float xb1 = mem1 ? xb1v : 0.0f;
 
   // ---- hand-off: trailing rows (coalesced by column), T and the vectors' prefix ----------
@@ -101,11 +103,13 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     A[col] = w[HO::TA + col * KT + l];
   });
   double u1t = w[HO::U1 + J0 + l], u2t = w[HO::U2 + J0 + l];  // trailing Q^T b1, Q^T x'
-  sm.tq[l][0] = w[HO::D + l];
-  sm.tq[l + 1][1] = w[HO::E + l];
-  sm.tq[l][2] = w[HO::U1 + l];
-  sm.tq[l][3] = w[HO::U2 + l];
-  sm.tau[l] = w[HO::TAU + l];
+  if (mem0) {
+    sm.tq[l][0] = w[HO::D + l];
+    sm.tq[l + 1][1] = w[HO::E + l];
+    sm.tq[l][2] = w[HO::U1 + l];
+    sm.tq[l][3] = w[HO::U2 + l];
+    sm.tau[l] = w[HO::TAU + l];
+  }
   // trailing rows of T: decoupled unit rows until the steps write them (rows >= k stay so)
   sm.tq[J0 + l][0] = 1.0;
   sm.tq[J0 + l + 1][1] = 0.0;
@@ -302,9 +306,11 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   }
   __syncthreads();
   // rows l (slot 0) and J0 + l (slot 1) in walk order: side 1 walks KP-1 .. H
-  const int w1 = H + (KP - 1 - (J0 + l));
-  double y0 = sm.Ym[l], y1 = sm.Ym[w1];
-  const double d = wave_sum_dpp(fma(sm.tq[l][2], sm.Zm[l], sm.tq[J0 + l][2] * sm.Zm[w1]));
+  auto walk = [](int i) { return i < H ? i : H + (KP - 1 - i); };
+  const int w0 = walk(mem0 ? l : 0), w1 = walk(J0 + l);
+  double y0 = mem0 ? sm.Ym[w0] : 0.0, y1 = sm.Ym[w1];
+  const double d = wave_sum_dpp(fma(mem0 ? sm.tq[l][2] : 0.0, sm.Zm[w0],
+                                    sm.tq[J0 + l][2] * sm.Zm[w1]));
   if (c.debug_stop == 3) {  // timing ablation: stop after the quadrature
     if (l == 0) info[gi] = make_int2(ptot, (int)(d + y0 + y1));
     return;
@@ -349,7 +355,7 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     sfor<4>([&](auto qq) {
       const int j = top - 3 + qq;
       const double h0 = w[HO::HV + j * KP + l];
-      v0[qq] = l > j ? h0 : 0.0;  // row j + 1 holds 1.0
+      v0[qq] = mem0 && l > j ? h0 : 0.0;  // row j + 1 holds 1.0
       v1[qq] = w[HO::HV + j * KP + J0 + l];
       ta[qq] = sm.tau[j];
     });
@@ -418,7 +424,7 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     xa0 = xa_mean + xap0;
     xa1 = xa_mean + xap1;
   }
-  slab.var[P + slab.L * l] = xa0;
+  if (mem0) slab.var[P + slab.L * l] = xa0;
   if (mem1) slab.var[P + slab.L * (J0 + l)] = xa1;
   // info.y: decade of the quadrature rule (negative when M/m exceeds the last table)
   if (l == 0) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
@@ -427,10 +433,14 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
 hipError_t launch_solve_tqb_tail(hipStream_t s, int kp, SolveConsts c, SlabDev slab,
                                  long long g0, int npts, double *ws, int2 *info) {
   if (npts <= 0) return hipSuccess;
-  if (c.quad == nullptr || kp != kBigSplitKP || c.k <= kBigJ0 + 2) return hipErrorInvalidValue;
+  if (c.quad == nullptr || (kp != 96 && kp != 128) || c.k <= kp - 62) return hipErrorInvalidValue;
   // (3 waves per SIMD, 168 VGPRs, spills 35 registers: 2.88 s per C4 variable against 2.57)
-  hipLaunchKernelGGL((solve_tqb_tail_kernel<kBigSplitKP, kBigJ0, 2>), dim3(npts), dim3(64), 0, s,
-                     c, slab, g0, npts, ws, info);
+  if (kp == 128)
+    hipLaunchKernelGGL((solve_tqb_tail_kernel<128, 64, 2>), dim3(npts), dim3(64), 0, s, c, slab,
+                       g0, npts, ws, info);
+  else
+    hipLaunchKernelGGL((solve_tqb_tail_kernel<96, 32, 2>), dim3(npts), dim3(64), 0, s, c, slab,
+                       g0, npts, ws, info);
   return hipGetLastError();
 }
 

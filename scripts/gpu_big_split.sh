@@ -3,7 +3,7 @@
 # tests, then the C4 bench split and one-kernel, then a kernel-trace profile of the split
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-[ "$TESTK" = none ] || timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "${TESTK:-kp128 or large_ensemble or c4_full}" > gpurun_out/pytest_split.log 2>&1
+[ "$TESTK" = none ] || timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "${TESTK:-split_big or large_ensemble or c4_full}" > gpurun_out/pytest_split.log 2>&1
 rc=$?; [ "$TESTK" = none ] || tail -12 gpurun_out/pytest_split.log
 [ $rc -eq 0 ] || { grep -E "Error|assert" gpurun_out/pytest_split.log | head -20; exit $rc; }
 for sp in ${SPLITS:-1 0}; do

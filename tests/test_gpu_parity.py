@@ -433,12 +433,12 @@ def test_large_ensemble_block_vs_oracle(k):
     assert rel <= INCR_TOL, rel
 
 
-@pytest.mark.parametrize("k,sparse", [(97, False), (101, True), (127, False), (128, False),
-                                      (128, True)])
-def test_split_kp128_path_vs_one_kernel_and_oracle(k, sparse, monkeypatch):
-    """The KP = 128 slab path runs split by default: solve_tq_big_kernel<128, false, 64>
-    (256 threads per point) hands the trailing 64x64 matrix and its 64 reflectors to
-    solve_tqb_tail_kernel (one point per wavefront).  k < 128 exercises the identity padding;
+@pytest.mark.parametrize("k,sparse", [(65, False), (80, True), (96, False), (97, False),
+                                      (101, True), (127, False), (128, False), (128, True)])
+def test_split_big_path_vs_one_kernel_and_oracle(k, sparse, monkeypatch):
+    """The KP = 96 / 128 slab paths run split by default: solve_tq_big_kernel<KP, false,
+    KP - 64> (256 threads per point) hands the trailing 64x64 matrix and its reflectors to
+    solve_tqb_tail_kernel (one point per wavefront).  k < KP exercises the identity padding;
     the sparse obs set gives points with p < k (rank-deficient Yb Yb^T, exactly-zero
     reflectors, tau = 0).  Against the one-kernel path (CWBL_BIG_SPLIT=0) on the whole
     30x30x50 grid and the oracle on a 5x5-column block; hand-off batches of 1024 points."""
@@ -552,7 +552,7 @@ def test_large_k_random_batch_vs_oracle(k):
         assert rel <= INCR_TOL, (p, rel)
 
 
-@pytest.mark.parametrize("name", ["c2", "c5", "driver_mixed.npz", "driver_c1.npz"])
+@pytest.mark.parametrize("name", ["c2", "c2_far", "c5", "driver_mixed.npz", "driver_c1.npz"])
 def test_binned_search_equals_tree_search(name, monkeypatch):
     """The analysis search runs on uniform bins (search_binned_kernel) with the k-d tree as
     the fallback where max_lz truncates (Q4).  The neighbour SETS are identical, so the solved
@@ -568,7 +568,13 @@ def test_binned_search_equals_tree_search(name, monkeypatch):
         slabs = lambda: case.slab()  # noqa: E731
         var_in = case.var_in
     else:
-        w = synth.make(name, scale=0.12 if name == "c2" else 0.04)
+        w = synth.make(name[:2], scale=0.04 if name == "c5" else 0.12)
+        if name == "c2_far":  # a domain 5000 km off the projection origin, 1.5 km localisation
+            w.x = w.x + np.float32(5e6)
+            w.y = w.y - np.float32(4e6)
+            w.obs_xyz = w.obs_xyz + np.array([5e6, -4e6, 0.0], np.float32)
+            for tp in w.vp.radar:
+                tp.hclr = tp.hclr / 8.0
         ob = lambda: abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs,  # noqa: E731
                                                     w.hdxb).build()
         mk = lambda: (abi.Core(w.k, device=0), ob(), w.vp)  # noqa: E731
