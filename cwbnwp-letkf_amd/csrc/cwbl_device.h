@@ -397,6 +397,113 @@ __device__ __forceinline__ int stage_columns(
   return ptot;
 }
 
+// stage_columns for the 256-thread kernels (analysis path) with two chunk buffers: the
+// gathers of chunk c + 1 are issued before chunk c is accumulated and committed (weights,
+// LDS writes) to the other buffer after it, so their latency hides behind the matrix cores;
+// one barrier per chunk.  Same columns, order and arithmetic as stage_columns;
+// accumulate(nsl, chunk) reads the chunk to accumulate.
+template <int KP, int CHUNK, int NT, class Acc>
+__device__ __forceinline__ int stage_columns_pipe(
+    ColumnChunk<KP, CHUNK> (&ch)[2], const TreeDesc *__restrict__ trees, const SolveConsts &c,
+    int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
+    const float3 pt, Acc &&accumulate) {
+  static_assert(NT > 64 && NT % CHUNK == 0 && CHUNK <= 64, "threads per staged column");
+  constexpr int LPC = NT / CHUNK;     // threads per staged column
+  constexpr int VH = KP / (2 * LPC);  // float2 of the bg row per thread
+  static_assert(KP % (4 * LPC) == 0, "bg row split into 16-B loads");
+  int ptot = 0;
+  if (lane < 32) ch[0].expt[lane] = kExpT[lane];
+  __syncthreads();  // (LDS is not cleared between workgroups)
+  const int sl = lane % CHUNK, half = lane / CHUNK;
+  int cur = 0;
+  for (int t = 0; t < c.ntrees; ++t) {
+    const TreeDesc T = trees[t];
+    const float q0 = pt.x * T.hclr_inv, q1 = pt.y * T.hclr_inv;  // get_lz (:243-253)
+    const float q2 = T.query3d ? pt.z * T.vclr_inv : 0.0f;
+    const int cnt = gptr(nbr_cnt)[(long long)gi * c.ntrees + t];
+    const int nvar = T.nvar;
+    const int npairs = cnt * nvar;
+    if (npairs == 0) continue;
+    const int *__restrict__ lst = nbr_idx + list_index(gi, c.list_cap, T.list_off);
+    const float rnv = 1.0f / (float)nvar;
+    auto divn = [&](int q) {
+      if (nvar == 1) return q;
+      int j = (int)((float)q * rnv);
+      j -= j * nvar > q ? 1 : 0;
+      j += (j + 1) * nvar <= q ? 1 : 0;
+      return j;
+    };
+    auto slot_of = [&](int base) {  // this lane's slot of the chunk at base (0 past the list)
+      return sl < min(CHUNK, npairs - base) ? gld(lst, list_slot(divn(base + sl))) : 0;
+    };
+    struct Gath {
+      f32x4 g[VH / 2];
+      f32x4 rd;
+      float err, omm;
+      uint8_t okb;
+      bool live;
+    };
+    auto gather = [&](int base, int slot, Gath &G) {
+      G.live = sl < min(CHUNK, npairs - base);
+      const int q = base + sl;
+      const int jn = divn(q), v = q - jn * nvar;
+      const int col = slot * nvar + v;  // a valid table index even past the list (slot 0)
+      const unsigned b0 = (unsigned)(col * KP + 2 * VH * half);
+#pragma unroll
+      for (int i = 0; i < VH / 2; ++i) G.g[i] = gld4(T.col_bg, b0 + 4u * i);
+      G.okb = gld(T.col_ok, (unsigned)col);
+      G.err = gld(T.col_err, (unsigned)col);
+      G.omm = gld(T.col_omm, (unsigned)col);
+      G.rd = gld4(reinterpret_cast<const float *>(T.rdata), 4u * (unsigned)slot);
+    };
+    auto commit = [&](const Gath &G, ColumnChunk<KP, CHUNK> &dst) {
+      // Every gathered register is consumed here, unconditionally: a dead component (rd.w)
+      // would have its register reused at once, and a use the compiler sinks into a divergent
+      // branch leaves the load pending on the skipping path; either way a later write to
+      // the register waits for the load (vmcnt) and the gathers no longer overlap the MFMAs.
+#pragma unroll
+      for (int i = 0; i < VH / 2; ++i) asm volatile("" ::"v"(G.g[i]));
+      asm volatile("" ::"v"(G.rd), "v"(G.err), "v"(G.omm), "v"((int)G.okb));
+      const bool ok = G.live && G.okb != 0;
+      const float wv =
+          error_inv(c.weight_function, G.err, slot_r2(G.rd, T.tree_dim, q0, q1, q2), ch[0].expt);
+      const float w = ok ? wv : 0.0f;
+      const float yo = ok ? G.omm * wv : 0.0f;  // omm * error_inv (:451)
+      ptot += __popcll(__ballot(ok && half == 0));  // counted by wave 0
+      if (half == 0) dst.yo[sl] = yo;
+      float *d = &dst.yb[sl][2 * VH * half];
+#pragma unroll
+      for (int i = 0; i < VH / 2; ++i) {  // bg * error_inv (:452)
+        *reinterpret_cast<float2 *>(d + 4 * i) = make_float2(G.g[i].x * w, G.g[i].y * w);
+        *reinterpret_cast<float2 *>(d + 4 * i + 2) = make_float2(G.g[i].z * w, G.g[i].w * w);
+      }
+    };
+    int slot_n = slot_of(CHUNK);  // chunk 1's slots, loaded behind chunk 0's gathers
+    {
+      Gath G;
+      gather(0, slot_of(0), G);
+      commit(G, ch[cur]);
+    }
+    __syncthreads();
+    for (int base = 0; base < npairs; base += CHUNK) {
+      const int nsl = min(CHUNK, npairs - base);
+      const int nb = base + CHUNK;
+      Gath Gn;
+      int slot_nn = 0;
+      if (nb < npairs) {  // wave-uniform
+        gather(nb, slot_n, Gn);
+        slot_nn = slot_of(nb + CHUNK);
+      }
+      accumulate(nsl, ch[cur]);
+      if (nb < npairs) commit(Gn, ch[cur ^ 1]);
+      __syncthreads();  // chunk cur ^ 1 is written; everyone is done reading chunk cur
+      cur ^= 1;
+      slot_n = slot_nn;
+    }
+  }
+  return ptot;
+}
+
 // Column assembly on the VALU: thread L accumulates the 4x4 blocks L, L+NT, ... of the lower
 // block triangle of Yb Yb^T, and threads < KP the entries of Yb d.
 template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64, class E = float>

@@ -21,7 +21,10 @@
 namespace cwbl {
 
 constexpr int kBigThreads = 256;
-constexpr int kBigChunk = 32;
+// columns staged per chunk: 64 at KP = 128, so that a chunk's MFMA phase (two waves per
+// SIMD) is long enough to cover the next chunk's gathers (stage_columns_pipe)
+template <int KP>
+constexpr int kBigChunk = KP == 128 ? 64 : 32;
 
 // thread -> 4x4 blocks of the lower block triangle for the tridiagonalisation's benefit.
 // Blocks are numbered column-major over the triangle; block (bi, bj) is read and updated
@@ -65,7 +68,7 @@ struct BigSmem {
   static constexpr int NB = KP / 4;
   static constexpr int PLD = 4 * NB + 4;  // 2*PLD = 8*odd dwords: conflict-free row sums
   union {
-    ColumnChunk<KP, kBigChunk> ch;
+    ColumnChunk<KP, kBigChunk<KP>> ch[2];     // staged columns (two buffers: stage_columns_pipe)
     double pb[NB][PLD];                   // A v partials: pb[R][4c+r] = block (R,c), row r
   } u;
   double col[KP];                         // pivot column / reflector j (back-transform)
@@ -195,28 +198,51 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     f64x4 tile[NTW];
 #pragma unroll
     for (int t = 0; t < NTW; ++t) tile[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-    b1acc = 0.0;
+    double b1p[4] = {0.0, 0.0, 0.0, 0.0};
     const int m = lane & 15, kk = lane >> 4;
     const int offA = 16 * wave + m, offB = 16 * (7 - wave) + m;
     int offJ[NTW];
 #pragma unroll
     for (int t = 0; t < NTW; ++t) offJ[t] = 16 * (t <= wave ? t : t - wave - 1) + m;
-    ptot = stage_columns<KP, kBigChunk, ASSEMBLED, NT>(
-        sm.u.ch, trees, c, gi, tid, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in,
-        [&](int nsl) {
-          // columns past nsl are staged as zeros (a multiple of 4 stays inside the chunk)
-          for (int s0 = 0; s0 < nsl; s0 += 4) {
-            const float *ys = sm.u.ch.yb[s0 + kk];
-            const double a = (double)ys[offA], b = (double)ys[offB];
+    // columns past nsl are staged as zeros (a multiple of 4 stays inside the chunk)
+    // (debug_stop 12: staging only, timing ablation)
+    auto mfma_chunk = [&](int nsl, const ColumnChunk<KP, kBigChunk<KP>> &cb) {
+      // (software-pipelining the group loop, group g + 1's operand reads before group g's
+      // MFMAs, measured no faster: 2.52 s per C4 variable either way)
+      for (int s0 = 0; s0 < (c.debug_stop == 12 ? 0 : nsl); s0 += 4) {
+        const float *ys = cb.yb[s0 + kk];
+        const double a = (double)ys[offA], b = (double)ys[offB];
 #pragma unroll
-            for (int t = 0; t < NTW; ++t)
-              tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(t <= wave ? a : b,
-                                                             (double)ys[offJ[t]], tile[t], 0, 0, 0);
-          }
-          if (tid < KP)  // Yb d (row KP of [Yb; yo] does not fit the tile padding)
-            for (int s = 0; s < nsl; ++s)
-              b1acc = fma((double)sm.u.ch.yb[s][tid], (double)sm.u.ch.yo[s], b1acc);
-        });
+        for (int t = 0; t < NTW; ++t)
+          tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(t <= wave ? a : b, (double)ys[offJ[t]],
+                                                         tile[t], 0, 0, 0);
+      }
+      // Yb d (row KP of [Yb; yo] does not fit the tile padding): eight columns per round,
+      // their LDS reads issued together, four chains (the staged columns past nsl are zeros)
+      if (tid < KP) {
+        constexpr int CH = kBigChunk<KP>;
+        const int nr = (nsl + 7) / 8;
+        for (int r8 = 0; r8 < nr; ++r8) {
+          const float4 o0 = *reinterpret_cast<const float4 *>(&cb.yo[8 * r8]);
+          const float4 o1 = *reinterpret_cast<const float4 *>(&cb.yo[8 * r8 + 4]);
+          const float o[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+          float y[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) y[i] = cb.yb[8 * r8 + i][tid];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) b1p[i & 3] = fma((double)y[i], (double)o[i], b1p[i & 3]);
+        }
+        static_assert(CH % 8 == 0, "Yb d rounds");
+      }
+    };
+    if constexpr (!ASSEMBLED)
+      ptot = stage_columns_pipe<KP, kBigChunk<KP>, NT>(sm.u.ch, trees, c, gi, tid, nbr_cnt, nbr_idx,
+                                                   pt, mfma_chunk);
+    else
+      ptot = stage_columns<KP, kBigChunk<KP>, ASSEMBLED, NT>(
+          sm.u.ch[0], trees, c, gi, tid, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in,
+          [&](int nsl) { mfma_chunk(nsl, sm.u.ch[0]); });
+    b1acc = (b1p[0] + b1p[1]) + (b1p[2] + b1p[3]);
     // block (bi, bj) lies in tile (I, J) = (bi/4, bj/4), held by wave min(I, 7-I) as its
     // tile t = J (I <= 3) or 8 - I + J (I >= 4); staged in round t/4, slot 4 wave + t%4
     int rnd[NBL], off[NBL];
@@ -258,7 +284,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
       }
     }
   } else {
-    assemble_point<KP, kBigChunk, ASSEMBLED, NT>(sm.u.ch, trees, c, gi, tid, nbr_cnt, nbr_idx,
+    assemble_point<KP, kBigChunk<KP>, ASSEMBLED, NT>(sm.u.ch[0], trees, c, gi, tid, nbr_cnt, nbr_idx,
                                                  pt, col_off, yo_in, yb_in, bi, bj, acc, b1acc,
                                                  ptot);
   }
@@ -273,7 +299,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     return;
   }
 
-  if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the rest
+  if (c.debug_stop == 1 || c.debug_stop == 12) {  // timing ablation: assembly only
     double t = b1acc;
 #pragma unroll
     for (int it = 0; it < NBL; ++it) t += acc[it][0] + acc[it][15];
