@@ -118,7 +118,7 @@ struct State {
   DevBuf flags;                                       // binned search: flagged points (+ count)
   bool binned = true;                                 // CWBL_SEARCH=tree: k-d tree search only
   bool jacobi = false;                                // CWBL_SOLVER=jacobi: eigen path
-  bool tq4 = true;                                    // CWBL_TQ4=0: one-kernel KP=40 solve
+  int tq4 = 1;  // CWBL_TQ4: KP=40 solve 0 = one kernel, 1 = assembly + tq40, 8 = hand-off after 8 steps
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: hand-off batch (points)
   bool big_split = true;                              // CWBL_BIG_SPLIT=0: one-kernel KP=128 solve
   long long big_sub = 32768;                          // CWBL_BIG_SUB: KP=128 hand-off batch
@@ -406,8 +406,8 @@ int cwbl_init(const cwbl_init_params *p) {
   }
   const char *solver = std::getenv("CWBL_SOLVER");
   S.jacobi = solver && std::strcmp(solver, "jacobi") == 0;
-  S.tq4 = true;
-  if (const char *e = std::getenv("CWBL_TQ4")) S.tq4 = std::atoi(e) != 0;
+  S.tq4 = 1;
+  if (const char *e = std::getenv("CWBL_TQ4")) S.tq4 = std::atoi(e);
   if (const char *e = std::getenv("CWBL_TQ4_SUB")) S.tq4_sub = std::atoll(e);
   S.big_split = true;
   S.big_sub = 32768;
@@ -676,14 +676,24 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       long long Bs = (nb + nsub - 1) / nsub;
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
       Bs = std::min<long long>(Bs, 1 << 19);
-      HIPCHK(S.wsa.ensure((size_t)Bs * Tq4Handoff<kTq4KP, kTq4J0>::WORDS * 8));
+      const bool rec = S.tq4 != 8;  // AsmRecord + solve_tq40_kernel, else Tq4Handoff
+      HIPCHK(S.wsa.ensure((size_t)Bs * 8 *
+                          (rec ? AsmRecord<kTq4KP>::WORDS : Tq4Handoff<kTq4KP, kTq4J0>::WORDS)));
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
         const int ns = (int)std::min<long long>(Bs, nb - s0);
-        HIPCHK(launch_assemble_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
-                                       ncnt + s0 * nt, nidx + s0 * list_cap,
-                                       S.info.as<int2>() + s0, S.wsa.as<double>()));
-        HIPCHK(launch_solve_tq4(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
-                                S.info.as<int2>() + s0));
+        if (rec) {
+          HIPCHK(launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
+                                        ncnt + s0 * nt, nidx + s0 * list_cap,
+                                        S.info.as<int2>() + s0, S.wsa.as<double>()));
+          HIPCHK(launch_solve_tq40(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
+                                   S.info.as<int2>() + s0));
+        } else {
+          HIPCHK(launch_assemble_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
+                                         ncnt + s0 * nt, nidx + s0 * list_cap,
+                                         S.info.as<int2>() + s0, S.wsa.as<double>()));
+          HIPCHK(launch_solve_tq4(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
+                                  S.info.as<int2>() + s0));
+        }
       }
     } else
       HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,

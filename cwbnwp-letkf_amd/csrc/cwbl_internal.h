@@ -191,6 +191,25 @@ hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees,
 hipError_t launch_solve_tq4(hipStream_t s, int kp, SolveConsts c, SlabDev slab, long long g0,
                             int npts, const double *ws, int2 *info);
 
+// The default KP = 40 split: assemble_record_kernel (cwbl_tq.hip) only stages and assembles,
+// one point per wavefront, and writes A = inflat I + Yb Yb^T (packed lower, the padding's
+// diagonal 1) and b1 = Yb d; solve_tq40_kernel (cwbl_tq40.hip) runs the whole
+// tridiagonalisation with four points per wavefront (the first kTq40J0 steps on full rows
+// J0..KP-1 plus the prefix rows' top-left block, then the same layout as solve_tq4_kernel),
+// solves and writes var in place.
+constexpr int kTq40J0 = 8;
+template <int KP>
+struct AsmRecord {
+  static constexpr int TA = 0;                   // A(r, c), c <= r, at r (r + 1) / 2 + c
+  static constexpr int U1 = KP * (KP + 1) / 2;   // b1 = Yb d (KP)
+  static constexpr int WORDS = (U1 + KP + 1) / 2 * 2;
+};
+hipError_t launch_assemble_record(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
+                                  SlabDev slab, long long g0, int npts, const int *nbr_cnt,
+                                  const int *nbr_idx, int2 *info, double *ws);
+hipError_t launch_solve_tq40(hipStream_t s, int kp, SolveConsts c, SlabDev slab, long long g0,
+                             int npts, const double *ws, int2 *info);
+
 // Split form of the KP = 128 slab path (configs[3]: k = 97..128).  solve_tq_big_kernel<128,
 // false, kBigJ0> assembles A and runs the first kBigJ0 Householder steps (4x4 register
 // blocks over 256 threads, one point per workgroup), then hands the trailing

@@ -671,6 +671,71 @@ hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees,
   return hipGetLastError();
 }
 
+// Stage + assemble only (the default KP = 40 split): the MFMA tiles of [Yb; yo][Yb; yo]^T go
+// straight from their C/D registers (row = 16 I + (lane >> 4) + 4 r, col = 16 J + (lane & 15))
+// to the record, packed lower, with inflat on the live diagonal and 1 on the padding's
+// (decoupled unit rows, as solve_tq_kernel's blocks); row KP of the product is b1 = Yb d.
+template <int KP>
+__global__ void __launch_bounds__(64, 4)
+assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
+                       long long g0, int npts, const int *__restrict__ nbr_cnt,
+                       const int *__restrict__ nbr_idx, int2 *__restrict__ info,
+                       double *__restrict__ ws) {
+  using L = MfmaLayout<KP>;
+  using HO = AsmRecord<KP>;
+  static_assert(L::YO_ROW, "b1 rides in the padding row");
+  __shared__ ColumnChunk<KP, kTqChunk, TqStage, L::PITCH> ch;
+  const int gi = xcd_remap(blockIdx.x, gridDim.x);
+  if (gi >= npts) return;
+  const int lane = threadIdx.x;
+  float3 pt;
+  slab_point(slab, g0 + gi, pt.x, pt.y, pt.z);
+  f64x4 tile[L::NTL];
+  double b1acc;
+  int ptot;
+  assemble_point_mfma<KP, kTqChunk, false>(ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt,
+                                           nullptr, nullptr, nullptr, tile, b1acc, ptot);
+  if (lane == 0) info[gi] = make_int2(ptot, 0);  // p = 0: the solve leaves var unchanged
+  if (ptot == 0) return;
+  if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the record
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < L::NTL; ++q) t += tile[q][0] + tile[q][3];
+    if (lane == 0) info[gi] = make_int2(ptot, (int)t);
+    return;
+  }
+  const int k = c.k;
+  const double inflat = (double)c.inflat;
+  double *__restrict__ w = ws + (long long)gi * HO::WORDS;
+  int t = 0;
+#pragma unroll
+  for (int I = 0; I < L::NT; ++I)
+#pragma unroll
+    for (int J = 0; J <= I; ++J, ++t) {
+      const int col = 16 * J + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * I + (lane >> 4) + 4 * r;
+        if (row < KP && col <= row) {
+          const double a = tile[t][r];
+          w[HO::TA + row * (row + 1) / 2 + col] = row != col ? a : row < k ? a + inflat : 1.0;
+        } else if (row == KP && col < KP) {
+          w[HO::U1 + col] = tile[t][r];
+        }
+      }
+    }
+}
+
+hipError_t launch_assemble_record(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
+                                  SlabDev slab, long long g0, int npts, const int *nbr_cnt,
+                                  const int *nbr_idx, int2 *info, double *ws) {
+  if (npts <= 0) return hipSuccess;
+  if (kp != kTq4KP) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((assemble_record_kernel<kTq4KP>), dim3(npts), dim3(64), 0, s, trees, c,
+                     slab, g0, npts, nbr_cnt, nbr_idx, info, ws);
+  return hipGetLastError();
+}
+
 template <int KP>
 static hipError_t launch_tq_kp(hipStream_t s, bool assembled, const TreeDesc *trees,
                                SolveConsts c, SlabDev slab, long long g0, int npts,

@@ -1,0 +1,593 @@
+// cwbl_tq40.hip — solve_tq40_kernel<KP>: the per-point LETKF solve (letkf_solve,
+// module_letkf_core.f90:598-700) from an assembled A, four grid points per wavefront.
+//
+// assemble_record_kernel (cwbl_tq.hip) stages the point's columns and forms
+// A = (k-1)/infl I + Yb Yb^T and b1 = Yb d on the matrix cores, one point per wavefront,
+// and writes them to the workspace (AsmRecord).  This kernel runs everything else of the
+// algorithm of solve_tq_kernel — the Householder tridiagonalisation A = Q T Q^T (dsytd2
+// order) applied on the fly to b1 and x', the T^-1/2 quadrature and the T^-1 solve, the
+// back-transform and the RTPP/RTPS epilogue in the reference's fp32 order — with
+//
+//   one 16-lane DPP row per point (q = lane / 16); lane l holds the FULL rows J0 + l and
+//   J0 + 16 + l of A (slots 0, 1; all KP columns) in registers, and lane l < J0 the
+//   top-left J0 x J0 block's row l (the prefix block).
+//
+// Rows 0..J0-1 of A are never held as rows: their entries right of column J0-1 are the
+// slots' columns 0..J0-1 (A is symmetric), which the slots' own rank-2 updates keep
+// current.  So during the first J0 steps (phase 1):
+//   - the pivot column j is register j of every slot row and of the prefix block;
+//   - (A v)_i of a prefix row i is its prefix-block part plus the column sum
+//     sum_c A(c, i) v_c over the slot rows (one 16-lane reduction per prefix row);
+//   - the update of the slots covers columns j+1 .. KP-1, which includes the prefix rows'
+//     entries right of the block; the block itself is updated on lanes < J0.
+// After J0 steps the trailing (KP-J0)^2 matrix sits in exactly the layout of
+// solve_tq4_kernel's steps (phase 2), and every reflector stays in the registers of the
+// column it eliminated (slot columns j, prefix register j), so nothing of the
+// tridiagonalisation goes through memory.  Every loop over steps, slots and columns is
+// compile-time (sfor), so all register indices are static.
+#include "cwbl_device.h"
+
+#include <utility>
+
+namespace cwbl {
+
+namespace {
+
+template <int... Is, class F>
+__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, Is...>, F &&f) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>), in order
+template <int N, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+  sfor_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+// value of lane L of this lane's 16-lane row (DPP row_newbcast; one v_mov_b64 for fp64,
+// bound_ctrl: every source lane is active)
+template <int L>
+__device__ __forceinline__ double rbcast(double x) {
+  return __longlong_as_double(
+      __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x150 + L, 0xf, 0xf, true));
+}
+template <int L>
+__device__ __forceinline__ float rbcast(float x) {
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x150 + L, 0xf, 0xf, true));
+}
+// value of lane l ^ 8 of the row (row_ror:8)
+__device__ __forceinline__ double ror8(double x) { return dpp_f64<0x128>(x); }
+
+}  // namespace
+
+template <int KP>
+struct Tq40Smem {
+  static constexpr int QLD = 9;  // 8 nodes per quadrature round (+1 against bank conflicts)
+  double qx[4][KP][QLD];         // per round: omega_n x_n(row) of the 8 nodes
+  double tq[4][KP + 1][4];       // d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
+  double tau[4][KP];
+};
+
+template <int KP>
+__global__ void __launch_bounds__(64, 2)
+solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
+                  const double *__restrict__ ws, int2 *__restrict__ info) {
+  using HO = AsmRecord<KP>;
+  constexpr int J0 = kTq40J0;         // steps with the prefix block (phase 1)
+  constexpr int KT = KP - J0;         // slot rows J0 + l + 16 r
+  constexpr int NS = KT / 16;         // row slots per lane
+  constexpr int NV = NS + 1;          // vector slots: 0 = rows l < J0, 1.. = row slots
+  constexpr int H = KP / 2;           // rows walked by each side of a twisted solve
+  static_assert(KT % 16 == 0 && J0 <= 16 && J0 >= 2 && KP % 2 == 0, "tq40 layout");
+  using SM = Tq40Smem<KP>;
+  __shared__ SM sm;
+
+  const int lane = threadIdx.x, q = lane >> 4, l = lane & 15;
+  const int gi = 4 * blockIdx.x + q;
+  const bool valid = gi < npts;
+  const int k = c.k;
+  const int ptot = valid ? info[gi].x : 0;
+  // record words of this point: SGPR base + 32-bit offset (the host keeps a batch's records
+  // below 2^32 bytes)
+  const unsigned wb = (unsigned)(valid ? gi : 0) * (unsigned)HO::WORDS;
+  auto w = [&](int i) { return gld(ws, wb + (unsigned)i); };
+  auto apk = [](int r, int col) {  // packed lower index of A(r, col)
+    return col <= r ? r * (r + 1) / 2 + col : col * (col + 1) / 2 + r;
+  };
+  // global row of vector slot vs (rows that do not exist get KP + 1: never < k)
+  auto vrow = [&](int vs) { return vs == 0 ? (l < J0 ? l : KP + 1) : J0 + l + 16 * (vs - 1); };
+
+  // var index of member 0 (g = i + ix_lim (j + iy_lim kz); g < 2^32: var would exceed HBM first)
+  long long P = 0;
+  {
+    const unsigned g = (unsigned)(g0 + (valid ? gi : 0));
+    const unsigned ix = (unsigned)slab.ix_lim, iy = (unsigned)slab.iy_lim;
+    const unsigned rr = g / ix, ii = g - rr * ix, kz = rr / iy, jj = rr - kz * iy;
+    P = ii + (long long)slab.nx * (jj + (long long)slab.ny * kz);
+  }
+
+  // ---- background of the point: member i = row i --------------------------------------------
+  float xbl[NV];
+  sfor<NV>([&](auto vv) {
+    constexpr int vs = decltype(vv)::value;
+    const int i = vrow(vs);
+    const bool mem = valid && i < k;
+    const float xv = slab.var[P + slab.L * (mem ? i : 0)];  // branch-free: a valid address
+    xbl[vs] = mem ? xv : 0.0f;
+  });
+  // fp32 sum over members in member order; member m is row m: prefix slot lane m (m < J0),
+  // else row slot (m - J0) / 16, lane (m - J0) % 16
+  auto seq_sum_f32 = [&](const float (&x)[NV]) {
+    float s = 0.0f;
+    sfor<KP>([&](auto mm) {
+      constexpr int m = decltype(mm)::value;
+      constexpr int vs = m < J0 ? 0 : 1 + (m - J0) / 16, ln = m < J0 ? m : (m - J0) % 16;
+      const float b = rbcast<ln>(x[vs]);
+      s = s + (m < k ? b : 0.0f);  // s + 0 = s: s is never -0
+    });
+    return s;
+  };
+  // sum(xb) * nmember_inv (:671)
+  const double xb_mean = (double)(seq_sum_f32(xbl) * c.nmember_inv);
+
+  // ---- A from the record (L2/MALL-resident, written just before) -----------------------------
+  double A[NS][KP];  // slot rows, all columns
+  sfor<NS>([&](auto rr) {
+    constexpr int r = decltype(rr)::value;
+    const int t = J0 + l + 16 * r;
+    sfor<KP>([&](auto cc) {
+      constexpr int col = decltype(cc)::value;
+      A[r][col] = w(HO::TA + apk(t, col));
+    });
+  });
+  double Pb[J0];  // prefix block row l (lanes >= J0 hold row 0's copy, never used)
+  const int lp = l < J0 ? l : 0;
+  const bool pre = l < J0;
+  sfor<J0>([&](auto cc) {
+    constexpr int col = decltype(cc)::value;
+    Pb[col] = w(HO::TA + apk(lp, col));
+  });
+  // x' (fp64, :671-672) and b1 = Yb d; both become Q^T x', Q^T b1
+  double uxP, ubP, ux[NS], ub[NS];
+  {
+    const double b = w(HO::U1 + lp);
+    ubP = pre ? b : 0.0;
+    uxP = pre && l < k ? (double)xbl[0] - xb_mean : 0.0;
+  }
+  sfor<NS>([&](auto rr) {
+    constexpr int r = decltype(rr)::value;
+    const int t = J0 + l + 16 * r;
+    ub[r] = w(HO::U1 + t);
+    ux[r] = t < k ? (double)xbl[r + 1] - xb_mean : 0.0;
+  });
+  double trace = 0.0;  // sum of d_j, j < k
+
+  // dlarfg with fp64 rcp/rsq refined to ~1 ulp; H = I when x = 0 (tau = 0, v = e_j+1)
+  struct Refl {
+    double beta, tau, scal;
+  };
+  auto dlarfg = [](double alpha, double xx) {
+    const double a2 = fma(alpha, alpha, xx);
+    const double rs = rsq64(a2);  // 1/|beta|
+    const bool nz = xx > 0.0;
+    const double bt = -copysign(a2 * rs, alpha);
+    Refl h;
+    h.beta = nz ? bt : alpha;
+    h.tau = nz ? (bt - alpha) * -copysign(rs, alpha) : 0.0;
+    const double rab = rcp64(alpha - bt);
+    h.scal = nz ? rab : 0.0;
+    return h;
+  };
+
+  // ---- phase 1: Householder steps 0 .. J0-1 with the prefix block -------------------------
+  sfor<J0>([&](auto jj) {
+    constexpr int j = decltype(jj)::value, J1 = j + 1;
+    const double dj = rbcast<j>(Pb[j]);  // A(j,j): final diagonal of T
+    trace += j < k ? dj : 0.0;
+    // alpha = A(j+1, j): prefix row j+1, or slot 0 lane 0 (row J0) at the last step
+    double alpha, u2a, u1a;
+    if constexpr (J1 < J0) {
+      alpha = rbcast<J1>(Pb[j]);
+      u2a = rbcast<J1>(uxP);
+      u1a = rbcast<J1>(ubP);
+    } else {
+      alpha = rbcast<0>(A[0][j]);
+      u2a = rbcast<0>(ux[0]);
+      u1a = rbcast<0>(ub[0]);
+    }
+    // x: column j below row j + 1 (rows < k)
+    const double xP = (pre && l > J1 && l < k) ? Pb[j] : 0.0;
+    double x[NS];
+    double xx = xP * xP, xu = xP * uxP, xb = xP * ubP;
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      const int i = J0 + l + 16 * r;
+      x[r] = (i > J1 && i < k) ? A[r][j] : 0.0;
+      xx = fma(x[r], x[r], xx);
+      xu = fma(x[r], ux[r], xu);
+      xb = fma(x[r], ub[r], xb);
+    });
+    xx = row16_sum(xx);
+    xu = row16_sum(xu);
+    xb = row16_sum(xb);
+    const Refl h = dlarfg(alpha, xx);
+    // every lane of the row writes the same value (no divergent branch in the step)
+    sm.tq[q][j][0] = dj;
+    sm.tq[q][J1][1] = h.beta;
+    sm.tau[q][j] = h.tau;
+    const double tau = h.tau;
+    // v: 1 at row j + 1, x * scal below; the reflector stays in column j's registers
+    const double xsP = xP * h.scal;
+    double vP = (pre && l == J1) ? 1.0 : xsP;
+    Pb[j] = xsP;
+    double v[NS];
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      const double xs = x[r] * h.scal;
+      if constexpr (J1 == J0 && r == 0) v[r] = l == 0 ? 1.0 : xs;
+      else v[r] = xs;
+      A[r][j] = xs;
+    });
+    const double s2 = fma(h.scal, xu, u2a);  // v . x'
+    const double s3 = fma(h.scal, xb, u1a);  // v . b1
+    uxP = fma(-tau * s2, vP, uxP);
+    ubP = fma(-tau * s3, vP, ubP);
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      ux[r] = fma(-tau * s2, v[r], ux[r]);
+      ub[r] = fma(-tau * s3, v[r], ub[r]);
+    });
+    // v_c of column c, wave-uniform per row: prefix lane c (c < J0) or its slot lane
+    auto vcol_of = [&](auto cc, const double &vp, const double (&vs)[NS]) {
+      constexpr int col = decltype(cc)::value;
+      if constexpr (col < J0) return rbcast<col>(vp);
+      else return rbcast<(col - J0) % 16>(vs[(col - J0) / 16]);
+    };
+    // A v: slot rows over columns j+1 .. KP-1; prefix rows = their block part + the column
+    // sums over the slot rows (A(i, c) = A(c, i) for c >= J0)
+    double p0[NS], p1[NS], pP = 0.0;
+    sfor<NS>([&](auto rr) { p0[decltype(rr)::value] = p1[decltype(rr)::value] = 0.0; });
+    sfor<KP - J1>([&](auto cc) {
+      constexpr int col = J1 + decltype(cc)::value;
+      const double vc = vcol_of(std::integral_constant<int, col>{}, vP, v);
+      sfor<NS>([&](auto rr) {
+        constexpr int r = decltype(rr)::value;
+        if constexpr ((col - J1) % 2 == 0) p0[r] = fma(A[r][col], vc, p0[r]);
+        else p1[r] = fma(A[r][col], vc, p1[r]);
+      });
+      if constexpr (col < J0) pP = fma(Pb[col], vc, pP);
+    });
+    sfor<J0 - J1>([&](auto cc) {  // prefix rows j+1 .. J0-1: column sums of the slots
+      constexpr int col = J1 + decltype(cc)::value;
+      double s = 0.0;
+      sfor<NS>([&](auto rr) {
+        constexpr int r = decltype(rr)::value;
+        s = fma(A[r][col], v[r], s);
+      });
+      s = row16_sum(s);
+      pP += l == col ? s : 0.0;
+    });
+    double pp[NS], sp = vP * pP;  // rows <= j: v = 0
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      pp[r] = p0[r] + p1[r];
+      sp = fma(v[r], pp[r], sp);
+    });
+    const double s1 = tau * row16_sum(sp);  // v^T (tau A v)
+    const double wP = (pre && l > j) ? fma(-0.5 * tau * s1, vP, tau * pP) : 0.0;
+    double wv[NS];
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      wv[r] = fma(-0.5 * tau * s1, v[r], tau * pp[r]);
+    });
+    // A <- A - v w^T - w v^T: slot rows over columns j+1 .. KP-1, the prefix block over
+    // columns j+1 .. J0-1.  (v is renamed first: otherwise the compiler reuses the matvec's
+    // broadcasts and keeps all KP - j of them live across the reduction, which spills.)
+    asm volatile("" : "+v"(vP));
+#pragma unroll
+    for (int r = 0; r < NS; ++r) asm volatile("" : "+v"(v[r]));
+    sfor<KP - J1>([&](auto cc) {
+      constexpr int col = J1 + decltype(cc)::value;
+      const double vc = vcol_of(std::integral_constant<int, col>{}, vP, v);
+      const double wc = vcol_of(std::integral_constant<int, col>{}, wP, wv);
+      sfor<NS>([&](auto rr) {
+        constexpr int r = decltype(rr)::value;
+        A[r][col] = fma(-v[r], wc, fma(-wv[r], vc, A[r][col]));
+      });
+      if constexpr (col < J0) Pb[col] = fma(-vP, wc, fma(-wP, vc, Pb[col]));
+    });
+  });
+  // the prefix rows of Q^T b1, Q^T x' are final (later reflectors vanish there)
+  if (pre) {
+    sm.tq[q][l][2] = ubP;
+    sm.tq[q][l][3] = uxP;
+  }
+
+  // ---- phase 2: steps J0 .. KP-3 on the trailing rows (solve_tq4_kernel's step) -----------
+  // Steps j >= k - 2 (k < KP) are exact no-ops: the padding rows and columns of A are the
+  // identity, so x = 0 there, tau = 0 and beta = A(j+1,j); running them keeps the code
+  // branch-free.
+  sfor<KT>([&](auto jj) {
+    constexpr int jl = decltype(jj)::value, j = J0 + jl;
+    constexpr int RJ = jl / 16, LJ = jl % 16;
+    const double dj = rbcast<LJ>(A[RJ][j]);  // A(j,j): final diagonal of T
+    trace += j < k ? dj : 0.0;
+    if constexpr (jl + 2 < KT) {
+      constexpr int J1 = jl + 1, R1 = J1 / 16, L1 = J1 % 16;
+      const double alpha = rbcast<L1>(A[R1][j]);
+      double x[NS], xx = 0.0, xu = 0.0, xb = 0.0;
+      sfor<NS>([&](auto rr) {
+        constexpr int r = decltype(rr)::value;
+        if constexpr (16 * r + 15 > J1) {
+          const int i = J0 + l + 16 * r;
+          x[r] = (i > j + 1 && i < k) ? A[r][j] : 0.0;
+          xx = fma(x[r], x[r], xx);
+          xu = fma(x[r], ux[r], xu);
+          xb = fma(x[r], ub[r], xb);
+        } else {
+          x[r] = 0.0;
+        }
+      });
+      xx = row16_sum(xx);
+      xu = row16_sum(xu);
+      xb = row16_sum(xb);
+      const Refl h = dlarfg(alpha, xx);
+      const double tau = h.tau;
+      sm.tq[q][j][0] = dj;
+      sm.tq[q][j + 1][1] = h.beta;
+      sm.tau[q][j] = tau;
+      double v[NS];
+      sfor<NS>([&](auto rr) {
+        constexpr int r = decltype(rr)::value;
+        const int t = l + 16 * r;
+        const double xs = x[r] * h.scal;
+        v[r] = t == J1 ? 1.0 : xs;
+        if constexpr (16 * r + 15 > J1) A[r][j] = xs;  // the reflector, rows > j + 1
+      });
+      const double s2 = fma(h.scal, xu, rbcast<L1>(ux[R1]));  // v . x'
+      const double s3 = fma(h.scal, xb, rbcast<L1>(ub[R1]));  // v . b1
+      sfor<NS>([&](auto rr) {
+        constexpr int r = decltype(rr)::value;
+        ux[r] = fma(-tau * s2, v[r], ux[r]);
+        ub[r] = fma(-tau * s3, v[r], ub[r]);
+      });
+      // A v over the trailing columns (v vanishes at columns <= j), column by column so
+      // that one broadcast v_c is live at a time
+      double p0[NS], p1[NS];
+      sfor<NS>([&](auto rr) { p0[decltype(rr)::value] = p1[decltype(rr)::value] = 0.0; });
+      sfor<KT - J1>([&](auto cc) {
+        constexpr int cl = J1 + decltype(cc)::value;
+        const double vcol = rbcast<cl % 16>(v[cl / 16]);
+        sfor<NS>([&](auto rr) {
+          constexpr int r = decltype(rr)::value;
+          if constexpr (16 * r + 15 > jl) {
+            if constexpr ((cl - J1) % 2 == 0) p0[r] = fma(A[r][J0 + cl], vcol, p0[r]);
+            else p1[r] = fma(A[r][J0 + cl], vcol, p1[r]);
+          }
+        });
+      });
+      double pp[NS], sp = 0.0;
+      sfor<NS>([&](auto rr) {
+        constexpr int r = decltype(rr)::value;
+        pp[r] = p0[r] + p1[r];
+        if constexpr (16 * r + 15 > jl) sp = fma(v[r], pp[r], sp);  // rows <= j: v = 0
+      });
+      const double s1 = tau * row16_sum(sp);  // v^T (tau A v)
+      double wv[NS];
+      sfor<NS>([&](auto rr) {
+        constexpr int r = decltype(rr)::value;
+        const int t = l + 16 * r;
+        wv[r] = t > jl ? fma(-0.5 * tau * s1, v[r], tau * pp[r]) : 0.0;
+      });
+      // A <- A - v w^T - w v^T on the trailing rows and columns (v renamed: fresh broadcasts)
+#pragma unroll
+      for (int r = 0; r < NS; ++r) asm volatile("" : "+v"(v[r]));
+      sfor<KT - J1>([&](auto cc) {
+        constexpr int cl = J1 + decltype(cc)::value;
+        const double vcol = rbcast<cl % 16>(v[cl / 16]);
+        const double wcol = rbcast<cl % 16>(wv[cl / 16]);
+        sfor<NS>([&](auto rr) {
+          constexpr int r = decltype(rr)::value;
+          if constexpr (16 * r + 15 > jl)
+            A[r][J0 + cl] = fma(-v[r], wcol, fma(-wv[r], vcol, A[r][J0 + cl]));
+        });
+      });
+    } else {  // the trailing 2x2: already tridiagonal (c(KP-2,KP-3) is step KP-3's beta)
+      const double ej = rbcast<LJ>(A[RJ][j - 1]);
+      sm.tq[q][j][0] = dj;
+      if constexpr (jl == KT - 1) sm.tq[q][j][1] = ej;
+    }
+  });
+  sfor<NS>([&](auto rr) {
+    constexpr int r = decltype(rr)::value;
+    const int i = J0 + l + 16 * r;
+    sm.tq[q][i][2] = ub[r];
+    sm.tq[q][i][3] = ux[r];
+  });
+  if (l == 0) {
+    sm.tq[q][0][1] = 0.0;
+    sm.tq[q][KP][1] = 0.0;
+  }
+  __syncthreads();
+
+  // ---- T^-1/2 u2 by quadrature, T^-1 u2 exactly --------------------------------------------
+  // lambda^-1/2 = (2/pi) int_0^inf dt / (t^2 + lambda) with the elliptic substitution and
+  // the midpoint rule on the spectrum bound [m, M] (solve_tq_kernel, cwbl_tq.hip): each node
+  // is one shifted SPD tridiagonal solve, twisted: lane l & 7 is the node of the round,
+  // side l >> 3 walks rows 0..H-1 (top) or KP-1..H (bottom); node 31 solves T^-1 u2.
+  const double m = (double)c.inflat;
+  const double ratio = trace / m - (double)(k - 1);
+  int level = 1;
+  double dec = 10.0;
+  while (level < kQuadLevels && dec < ratio) {
+    dec *= 10.0;
+    ++level;
+  }
+  const int side = l >> 3, n8 = l & 7;
+  const double(*T)[4] = sm.tq[q];
+  const double *tq0 = &T[side ? KP - 1 : 0][0];
+  const int dir = side ? -4 : 4;
+  const int cs = side ? 5 : 1;  // coupling with the previous row of the walk
+  double ys[NV], z[NV];
+  sfor<NV>([&](auto vv) { ys[decltype(vv)::value] = 0.0; });
+  for (int round = 0; round < 4; ++round) {
+    const int node = 8 * round + n8;
+    const double2 tw = c.quad[(level - 1) * 32 + min(node, kQuadNodes - 1)];
+    const double sigma = node < kQuadNodes ? m * tw.x : 0.0;
+    const double omega = node < kQuadNodes ? sqrt(m) * tw.y : 1.0;
+    double hh[H], mm[H];
+    double dl = tq0[0] + sigma, gt = tq0[3];
+    double rdl = rcp64(dl);
+    sfor<H - 1>([&](auto tt) {
+      constexpr int t = decltype(tt)::value + 1;
+      const double *qt = tq0 + dir * t;
+      const double ct = qt[cs];
+      const double lt = ct * rdl;
+      hh[t - 1] = gt * rdl;
+      mm[t - 1] = lt;
+      dl = fma(-lt, ct, qt[0] + sigma);
+      gt = fma(-lt, gt, qt[3]);
+      rdl = rcp64(dl);
+    });
+    // rows H-1 (top) and H (bottom): 2x2 solve with the partner lane's pivot
+    const double cm = T[H][1];
+    const double dlo = ror8(dl), go = ror8(gt);
+    double xv = (gt * dlo - cm * go) / fma(dl, dlo, -cm * cm);
+    auto row_of = [&](int t) { return side ? KP - 1 - t : t; };
+    sm.qx[q][row_of(H - 1)][n8] = omega * xv;
+    sfor<H - 1>([&](auto tt) {
+      constexpr int t = H - 2 - decltype(tt)::value;
+      xv = fma(-mm[t], xv, hh[t]);
+      sm.qx[q][row_of(t)][n8] = omega * xv;
+    });
+    __syncthreads();
+    const bool last = round == 3;  // node 31 (slot 7 of the last round) is T^-1 u2
+    sfor<NV>([&](auto vv) {
+      constexpr int vs = decltype(vv)::value;
+      const int i = vrow(vs);
+      const double *row = sm.qx[q][i < KP ? i : 0];
+      double s = 0.0;
+      sfor<7>([&](auto nn) { s += row[decltype(nn)::value]; });
+      const double r7 = row[7];
+      s = last ? s : s + r7;
+      ys[vs] += i < KP ? s : 0.0;
+      if (last) z[vs] = i < KP ? r7 : 0.0;
+    });
+    __syncthreads();
+  }
+  double dpart = 0.0;  // u1 . T^-1 u2 = wbar . x'
+  sfor<NV>([&](auto vv) {
+    constexpr int vs = decltype(vv)::value;
+    const int i = vrow(vs);
+    const double u1 = vs == 0 ? ubP : ub[vs > 0 ? vs - 1 : 0];
+    dpart = i < KP ? fma(u1, z[vs], dpart) : dpart;
+  });
+  const double d = row16_sum(dpart);
+
+  // ---- back-transform: y <- Q y = H_0 H_1 ... H_{KP-3} y ----------------------------------
+  double y[NV];
+  sfor<NV>([&](auto vv) { y[decltype(vv)::value] = ys[decltype(vv)::value]; });
+  sfor<KT - 2>([&](auto jj) {  // phase 2's reflectors (rows > J0 only)
+    constexpr int jl = KT - 3 - decltype(jj)::value, j = J0 + jl, J1 = jl + 1;
+    const double tj = sm.tau[q][j];
+    double vv[NS], a = 0.0;
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      if constexpr (16 * r + 15 >= J1) {
+        const int t = l + 16 * r;
+        vv[r] = t == J1 ? 1.0 : (t > J1 ? A[r][j] : 0.0);
+        a = fma(vv[r], y[r + 1], a);
+      } else {
+        vv[r] = 0.0;
+      }
+    });
+    a = row16_sum(a);
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      if constexpr (16 * r + 15 >= J1) y[r + 1] = fma(-tj * a, vv[r], y[r + 1]);
+    });
+  });
+  sfor<J0>([&](auto jj) {  // phase 1's reflectors: prefix register j and slot column j
+    constexpr int j = J0 - 1 - decltype(jj)::value, J1 = j + 1;
+    const double tj = sm.tau[q][j];
+    const double v0 = !pre ? 0.0 : l == J1 ? 1.0 : Pb[j];  // Pb[j] is 0 at rows <= j + 1
+    double vv[NS];
+    double a = v0 * y[0];
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      if constexpr (J1 == J0 && r == 0) vv[r] = l == 0 ? 1.0 : A[r][j];
+      else vv[r] = A[r][j];
+      a = fma(vv[r], y[r + 1], a);
+    });
+    a = row16_sum(a);
+    y[0] = fma(-tj * a, v0, y[0]);
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      y[r + 1] = fma(-tj * a, vv[r], y[r + 1]);
+    });
+  });
+
+  // ---- analysis and RTPP / RTPS (:675-698), fp32 in the reference's order ----------------
+  const double sk = sqrt((double)(k - 1));
+  float xa[NV];
+  sfor<NV>([&](auto vv) {
+    constexpr int vs = decltype(vv)::value;
+    xa[vs] = vrow(vs) < k ? (float)(xb_mean + (d + sk * y[vs])) : 0.0f;
+  });
+  if (c.use_rtpp || c.use_rtps) {
+    const float xa_mean = seq_sum_f32(xa) * c.nmember_inv;
+    double xpl[NV];
+    float xap[NV];
+    sfor<NV>([&](auto vv) {
+      constexpr int vs = decltype(vv)::value;
+      const bool mem = vrow(vs) < k;
+      xpl[vs] = mem ? (double)xbl[vs] - xb_mean : 0.0;
+      xap[vs] = 0.0f;
+      if (mem) {
+        xap[vs] = xa[vs] - xa_mean;
+        if (c.use_rtpp)
+          xap[vs] = (float)((double)((1.0f - c.rtpp_alpha) * xap[vs]) +
+                            (double)c.rtpp_alpha * xpl[vs]);
+      }
+    });
+    if (c.use_rtps) {
+      double d8 = 0.0;
+      sfor<KP>([&](auto mm) {
+        constexpr int mb = decltype(mm)::value;
+        constexpr int vs = mb < J0 ? 0 : 1 + (mb - J0) / 16, ln = mb < J0 ? mb : (mb - J0) % 16;
+        const double xp = rbcast<ln>(xpl[vs]);  // 0 past member k-1
+        d8 = d8 + xp * xp;
+      });
+      const float xb_std = (float)d8;
+      float sq[NV];
+      sfor<NV>([&](auto vv) {
+        constexpr int vs = decltype(vv)::value;
+        sq[vs] = xap[vs] * xap[vs];
+      });
+      const float xa_std = seq_sum_f32(sq);
+      const float f = c.rtps_alpha * sqrtf(xb_std / xa_std) - c.rtps_alpha + 1.0f;
+      sfor<NV>([&](auto vv) { xap[decltype(vv)::value] = xap[decltype(vv)::value] * f; });
+    }
+    sfor<NV>([&](auto vv) { xa[decltype(vv)::value] = xa_mean + xap[decltype(vv)::value]; });
+  }
+  if (valid && ptot > 0) {
+    sfor<NV>([&](auto vv) {
+      constexpr int vs = decltype(vv)::value;
+      const int i = vrow(vs);
+      if (i < k) slab.var[P + slab.L * i] = xa[vs];
+    });
+    // info.y: decade of the quadrature rule (negative when M/m exceeds the last table)
+    if (l == 0) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
+  }
+}
+
+hipError_t launch_solve_tq40(hipStream_t s, int kp, SolveConsts c, SlabDev slab, long long g0,
+                             int npts, const double *ws, int2 *info) {
+  if (npts <= 0) return hipSuccess;
+  if (c.quad == nullptr || kp != kTq4KP) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP>), dim3((npts + 3) / 4), dim3(64), 0, s, c, slab,
+                     g0, npts, ws, info);
+  return hipGetLastError();
+}
+
+}  // namespace cwbl

@@ -217,14 +217,16 @@ def test_synthetic_c2_subdomain_vs_oracle():
 
 @pytest.mark.parametrize("k", [33, 36, 40])
 def test_split_kp40_path_vs_one_kernel_and_oracle(k, monkeypatch):
-    """The KP = 40 slab path runs split by default (solve_tq_kernel<40, false, 8> hands the
-    trailing 32x32 matrix to solve_tq4_kernel, four points per wavefront); k < 40 exercises
-    the identity padding (the no-op steps past k - 2).  Against the one-kernel path
-    (CWBL_TQ4=0) and the oracle on a 30x30x50 C2-shaped grid."""
+    """The KP = 40 slab path runs split by default (assemble_record_kernel writes A and Yb d,
+    solve_tq40_kernel runs the whole tridiagonalisation four points per wavefront, CWBL_TQ4=1);
+    CWBL_TQ4=8 is the earlier split (solve_tq_kernel<40, false, 8> hands the trailing 32x32
+    matrix to solve_tq4_kernel).  k < 40 exercises the identity padding (the no-op steps past
+    k - 2).  Both against the one-kernel path (CWBL_TQ4=0) and the oracle on a 30x30x50
+    C2-shaped grid."""
     import ctypes as C
     w = _radar_case_scaled(0.1, k=k)
     out = {}
-    for mode in ("0", "1"):
+    for mode in ("0", "1", "8"):
         monkeypatch.setenv("CWBL_TQ4", mode)
         _cores.clear()
         c = abi.Core(w.k, device=0)
@@ -234,18 +236,19 @@ def test_split_kp40_path_vs_one_kernel_and_oracle(k, monkeypatch):
         c.finalize()
         assert st.nonconverged == 0 and st.solved > 0
         out[mode] = (var, st.solved, st.nobs_sum)
-    assert out["0"][1:] == out["1"][1:]
+    assert out["0"][1:] == out["1"][1:] == out["8"][1:]
     ref = w.var.copy()
     ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
     rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
                                   C.byref(abi.make_slab(w.x, w.y, w.alt, ref)), 16,
                                   C.byref(abi.Stats()))
     assert rc == 0
-    for mode in ("0", "1"):
+    for mode in ("0", "1", "8"):
         rel = increment_rel_rms(out[mode][0], ref, w.var)
         assert rel <= INCR_TOL, (mode, rel)
-    rel = increment_rel_rms(out["1"][0], out["0"][0], w.var)
-    assert rel <= INCR_TOL, rel
+    for mode in ("1", "8"):
+        rel = increment_rel_rms(out[mode][0], out["0"][0], w.var)
+        assert rel <= INCR_TOL, (mode, rel)
 
 
 def test_c2_full_size_properties():
