@@ -8,8 +8,9 @@ pass of the reference's per-variable hot loop (module_letkf_core.f90:63-64 + 209
 k-d tree builds, QC columns, neighbour search and the per-point LETKF solve for every grid
 point.  Inputs (obs set and slab) are resident in HBM before the timed region.
 
-Multi-GPU (launched by torch.distributed.run, one process per GPU): grid rows are dealt
-cyclically to ranks (block-1 decomposition as in module_mpi_util.f90:73-188); the observation
+Multi-GPU (launched by torch.distributed.run, one process per GPU): grid columns are dealt
+to ranks as the reference deals them (cyclic block-1 px x py grid, module_mpi_util.f90:71-188;
+300 x 300 splits evenly over 1, 2, 4 and 8 ranks); the observation
 set is generated on rank 0 and sent to every rank with ONE RCCL broadcast (backend "nccl")
 before the timed region; there is no collective on the data path.  The grid is fixed as N
 grows (configs[2]: the 300x300x50 grid sharded across GPUs), so scaling is "strong".
@@ -33,6 +34,7 @@ import torch.distributed as dist  # noqa: E402
 
 from cwbl import abi, synth  # noqa: E402
 from cwbl import dist as cdist  # noqa: E402
+from cwbl.transpose import dims_create as tr_dims  # noqa: E402
 
 METRIC = "analysis grid-points/sec (+ wall-clock per cycle) at k=40, 1/2/4/8 MI355X"
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector = matrix on gfx950), spec
@@ -191,7 +193,7 @@ CYCLE = (("U", 1.6, "u"), ("V", 1.6, "v"), ("W", 1.6, "w"), ("T", 1.6, "m"),
 
 
 def time_cycle(core, w, world, dev, x, y, alt):
-    """Wall-clock of one analysis cycle on this rank's rows: every var_update entry of
+    """Wall-clock of one analysis cycle on this rank's columns: every var_update entry of
     input.nml analysed with the configuration's obs set and localisation (one obs type, so
     the k-d trees are built once and shared, as the tree cache does for variables of equal
     localisation).  Slabs are made on the device before the timed region (synthetic
@@ -270,7 +272,7 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    w = synth.make(args.config, rows=(rank, world) if world > 1 else None)
+    w = synth.make(args.config, shard=(rank, world) if world > 1 else None)
     k = w.k
     # ---- observation set: packed on rank 0 (obs-set wire format), broadcast over RCCL --------
     n = w.obs.shape[0]
@@ -376,14 +378,15 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"{args.config}: {w.nx}x{w.extra['cfg']['ny']}x{w.nz} grid, k={k}, "
+                "workload": f"{args.config}: {w.extra['cfg']['nx']}x{w.extra['cfg']['ny']}x{w.nz} grid, k={k}, "
                             f"{n} {'radar-dbz' if w.radar_type == abi.RADAR_DBZ else 'radar-VR'}-like obs (hclr {w.extra['cfg']['hclr']} km, vclr "
                             f"{w.extra['cfg']['vclr']} km), RTPP+RTPS, Gaussian localisation",
                 "grid_points": int(w.extra["cfg"]["nx"] * w.extra["cfg"]["ny"] * w.nz),
                 "k": k,
                 "n_obs": n,
                 "mean_p": nobs_sum / max(solved, 1),
-                "parallelism": f"column-sharded x{world}" + (
+                "parallelism": f"column-sharded x{world} (px x py = "
+                               f"{'x'.join(map(str, tr_dims(world)))})" + (
                     ", obs-set broadcast over " + ("RCCL" if dist.get_backend() == "nccl"
                                                   else dist.get_backend())
                     if world > 1 else ""),

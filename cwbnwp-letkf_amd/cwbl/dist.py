@@ -4,19 +4,20 @@ The analysis shards embarrassingly: grid columns are dealt to ranks and points n
 communicate.  The only exchange is ONE broadcast of the packed observation set from the
 rank that read it (RCCL over xGMI on MI355X, backend "nccl"; gloo on CPU for tests).  It
 replaces the reference's ibcast/iallgatherv chain (module_gts_omboma.f90:524-611,
-module_radar.f90:143-180).  Rows are dealt cyclically with block 1, which balances the
-uneven obs density.  This row-only deal is NOT the reference's decomposition: that is a
-2-D px x py cyclic column grid (letkf_local_info, module_mpi_util.f90:71-188), reproduced
-by cwbl/transpose.py for the member<->column transposes.  Points are independent, so the
-analysis does not depend on which split is used.
+module_radar.f90:143-180).  Columns are dealt as the reference deals them: cyclically with
+block 1 over a px x py rank grid (letkf_local_info, module_mpi_util.f90:71-188, px >= py from
+MPI_Dims_create; cwbl/transpose.py's Decomposition), which balances the uneven obs density
+and gives every rank the same point count whenever px | nx and py | ny (300 x 300 over 1, 2,
+4 or 8 ranks).
 """
 import numpy as np
 
 
-def shard_rows(ny, rank, world):
-    """Grid rows j owned by `rank`: a row-only cyclic deal (block size 1), not
-    letkf_local_info's 2-D column grid."""
-    return np.arange(rank, ny, world)
+def shard_columns(nx, ny, rank, world):
+    """(xs, ys): the 0-based grid columns x and rows y of `rank`'s columns (cpu(rank)%xloc,
+    %yloc of letkf_local_info); the rank analyses the loc_nx x loc_ny block of their products."""
+    from .transpose import Decomposition
+    return Decomposition(nx, ny, world).columns(rank)
 
 
 # ---- wire format of a whole observation set (SURVEY.md §8(f) rank 3) ------------------------

@@ -65,11 +65,11 @@ def radar_var_params(hclr, vclr, max_lz, err, err_rej, radar_type, multi_infl=1.
                           rtps_alpha=0.95, radar={radar_type: tp})
 
 
-def make(name="c2", seed=20261015, scale=None, rows=None, **over):
+def make(name="c2", seed=20261015, scale=None, shard=None, **over):
     """Build a workload.  `scale` shrinks nx/ny (domain and obs count scale with it) for
-    tests; `rows` = (start, step) keeps grid rows j = start, start+step, ... (cyclic
-    sharding of the columns across ranks, like the reference's block-1 decomposition,
-    module_mpi_util.f90:73-188).  The obs set never depends on `rows`."""
+    tests; `shard` = (rank, world) keeps that rank's columns of the reference's cyclic
+    block-1 column grid (letkf_local_info, module_mpi_util.f90:71-188; dist.shard_columns).
+    The obs set never depends on `shard`."""
     cfg = dict(CONFIGS[name])
     cfg.update(over)
     if scale:
@@ -101,17 +101,18 @@ def make(name="c2", seed=20261015, scale=None, rows=None, **over):
         var[m] = tr + rng.standard_normal((nz, ny, nx), dtype=np.float32)
     x = X.astype(np.float32)
     y = Y.astype(np.float32)
-    if rows is not None:
-        from .dist import shard_rows
-        sel = shard_rows(ny, rows[0], rows[1])
+    if shard is not None:
+        from .dist import shard_columns
+        xs, ys = shard_columns(nx, ny, shard[0], shard[1])
+        sel = np.ix_(ys, xs)
         x, y = x[sel].copy(), y[sel].copy()
-        alt = alt[:, sel].copy()
-        var = var[:, :, sel].copy()
+        alt = np.ascontiguousarray(alt[:, ys][:, :, xs])
+        var = np.ascontiguousarray(var[:, :, ys][:, :, :, xs])
     vp = radar_var_params(cfg["hclr"], cfg["vclr"], cfg["max_lz"], cfg["err"], cfg["err_rej"],
                           cfg["radar_type"])
-    return Workload(name=name, k=k, nx=nx, ny=x.shape[0], nz=nz, x=x, y=y, alt=alt, var=var,
-                    radar_type=cfg["radar_type"], obs_xyz=oxyz, obs=obs, hdxb=hdxb, vp=vp,
-                    extra=dict(cfg=cfg, seed=seed, rows=rows))
+    return Workload(name=name, k=k, nx=x.shape[1], ny=x.shape[0], nz=nz, x=x, y=y, alt=alt,
+                    var=var, radar_type=cfg["radar_type"], obs_xyz=oxyz, obs=obs, hdxb=hdxb,
+                    vp=vp, extra=dict(cfg=cfg, seed=seed, shard=shard))
 
 
 def flops_per_point(k, p):

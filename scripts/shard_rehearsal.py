@@ -1,4 +1,5 @@
-# Rank 0's share of the C2 grid at world sizes 1, 2, 4, 8 (cyclic rows), timed alone on one
+# Rank 0's share of the C2 grid at world sizes 1, 2, 4, 8 (the reference's cyclic column
+# grid), timed alone on one
 # GPU: the per-rank step time the strong-scaling bench will see, without the collectives.
 import sys, time
 sys.path.insert(0, "cwbnwp-letkf_amd")
@@ -10,7 +11,7 @@ from cwbl import dist as cdist
 dev = torch.device("cuda", 0)
 base = None
 for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
-    w = synth.make("c2", rows=(0, world) if world > 1 else None)
+    w = synth.make("c2", shard=(0, world) if world > 1 else None)
     types = [dict(family=1, type_id=w.radar_type, xyz=w.obs_xyz, obs=w.obs, hdxb=w.hdxb)]
     _, types = cdist.unpack_obs_set(torch.from_numpy(cdist.pack_obs_set(types, w.k)).to(dev))
     x, y, alt = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt))

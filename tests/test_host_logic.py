@@ -21,11 +21,27 @@ def test_synthetic_c2_shapes_and_determinism():
     np.testing.assert_array_equal(a.hdxb, b.hdxb)
 
 
-def test_sharded_rows_are_slices_of_the_full_grid():
-    full = synth.make("c2", scale=0.05, nz=3)
-    part = synth.make("c2", scale=0.05, nz=3, rows=(1, 3))
-    np.testing.assert_array_equal(part.var, full.var[:, :, 1::3])
-    np.testing.assert_array_equal(part.obs, full.obs)
+def test_shards_are_the_reference_column_grid_of_the_full_grid():
+    # letkf_local_info (module_mpi_util.f90:71-188): rank r = ix + iy*px of a px x py grid
+    # (px >= py, MPI_Dims_create) owns columns x = ix + i*px, rows y = iy + j*py
+    full = synth.make("c2", scale=0.05, nz=3)  # 15 x 15
+    for world, (px, py) in ((1, (1, 1)), (3, (3, 1)), (4, (2, 2)), (6, (3, 2)), (8, (4, 2))):
+        seen = np.zeros((full.ny, full.nx), np.int32)
+        for r in range(world):
+            part = synth.make("c2", scale=0.05, nz=3, shard=(r, world))
+            ix, iy = r % px, r // px
+            np.testing.assert_array_equal(part.var, full.var[:, :, iy::py, ix::px])
+            np.testing.assert_array_equal(part.x, full.x[iy::py, ix::px])
+            np.testing.assert_array_equal(part.alt, full.alt[:, iy::py, ix::px])
+            np.testing.assert_array_equal(part.obs, full.obs)
+            seen[iy::py, ix::px] += 1
+        assert (seen == 1).all()
+    # 300 x 300 (configs[1..2]) splits evenly over 1, 2, 4 and 8 ranks
+    from cwbl.dist import shard_columns
+    for world in (1, 2, 4, 8):
+        sizes = {len(a) * len(b) for a, b in (shard_columns(300, 300, r, world)
+                                               for r in range(world))}
+        assert sizes == {90000 // world}
 
 
 def test_var_params_defaults_follow_module_config():

@@ -1,4 +1,5 @@
-"""Multi-process (world_size 2, gloo, CPU) check of the sharded path: rows dealt cyclically,
+"""Multi-process (world_size 2, gloo, CPU) check of the sharded path: columns dealt as the
+reference deals them (cyclic px x py grid),
 the obs set broadcast once from rank 0, each rank analysing its shard independently (with
 the oracle standing in for the GPU core on CPU), results reassembled == single process."""
 import ctypes as C
@@ -40,7 +41,7 @@ def _worker(rank, world, port, out_dir):
     sys.path.insert(0, os.path.join(repo, "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    w = synth.make("c2", seed=5, scale=0.06, nz=6, rows=(rank, world))
+    w = synth.make("c2", seed=5, scale=0.06, nz=6, shard=(rank, world))
     n, k = w.obs.shape[0], w.k
     buf = torch.zeros(cdist.packed_len(n, k), dtype=torch.float32)
     if rank == 0:
@@ -64,8 +65,8 @@ def test_sharded_analysis_equals_single_process(tmp_path):
     ref, solved_ref = _analyse_oracle(full, full.obs_xyz, full.obs, full.hdxb)
     got = np.empty_like(ref)
     for r in range(world):
-        rows = cdist.shard_rows(full.var.shape[2], r, world)
-        got[:, :, rows, :] = np.load(tmp_path / f"rank{r}.npy")
+        xs, ys = cdist.shard_columns(full.nx, full.ny, r, world)
+        got[:, :, ys[:, None], xs[None, :]] = np.load(tmp_path / f"rank{r}.npy")
     np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert int(np.load(tmp_path / "solved.npy")[0]) == solved_ref
 
@@ -143,11 +144,14 @@ def test_obs_set_wire_roundtrip():
         cdist.unpack_obs_set(bad)
 
 
-def test_shard_rows_partition():
-    for ny in (1, 7, 300):
+def test_shard_columns_partition():
+    for nx, ny in ((1, 1), (7, 5), (300, 300), (301, 299)):
         for world in (1, 2, 3, 8):
-            rows = np.concatenate([cdist.shard_rows(ny, r, world) for r in range(world)])
-            assert sorted(rows.tolist()) == list(range(ny))
+            seen = np.zeros((ny, nx), np.int32)
+            for r in range(world):
+                xs, ys = cdist.shard_columns(nx, ny, r, world)
+                seen[ys[:, None], xs[None, :]] += 1
+            assert (seen == 1).all()
 
 
 def test_pack_roundtrip():
