@@ -332,9 +332,12 @@ def main():
         flops = synth.flops_total(k, solved, nobs_sum)
         achieved = flops / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else 0.0
         kp = ((k + 7) // 8) * 8 if k <= 64 else (96 if k <= 96 else 128)
-        split = (not jacobi and kp == 40 and os.environ.get("CWBL_TQ4", "1") != "0")
+        tq4 = os.environ.get("CWBL_TQ4", "1")
+        split = not jacobi and kp == 40 and tq4 != "0"
         split128 = kp == 128 and k > 66 and os.environ.get("CWBL_BIG_SPLIT", "1") != "0"
-        kname = ("solve_tq_kernel<40, false, 8> + solve_tq4_kernel<40, 8>" if split else
+        kpair = (("assemble_record_kernel<40>", "solve_tq40_kernel<40>") if tq4 != "8" else
+                 ("solve_tq_kernel<40, false, 8>", "solve_tq4_kernel<40, 8>"))
+        kname = (" + ".join(kpair) if split else
                  "solve_tq_big_kernel<128, false, 64> + solve_tqb_tail_kernel<128, 64, 2>"
                  if split128 else
                  ("solve_kernel" if jacobi else
@@ -355,7 +358,7 @@ def main():
         if split and args.config == "c2" and os.path.exists(fl):
             with open(fl) as f:
                 fk = json.load(f)["kernels"]
-            ka, kb = "cwbl::solve_tq_kernel<40, false, 8>", "cwbl::solve_tq4_kernel<40, 8>"
+            ka, kb = ("cwbl::" + kn for kn in kpair)
             if ka in fk and kb in fk and ms_solve > 0:
                 per_pt = (fk[ka]["fp64_flops_per_launch"] + fk[kb]["fp64_flops_per_launch"]) / \
                     fk[ka]["counters_per_launch"]["SQ_WAVES"]
