@@ -89,7 +89,8 @@ struct SolveConsts {
   const double2 *quad;        // [kQuadLevels][32] (t2, w) of the x^-1/2 rule (solve_tq_kernel)
   int   stagger;              // CWBL_DEBUG_STAGGER: start-phase offset unit in cycles (experiment)
   int   debug_stop;           // CWBL_DEBUG_TQ_STOP: 1 = after assembly, 2 = after
-                              // tridiagonalisation, 3 = after quadrature (timing ablation only)
+                              // tridiagonalisation, 3 = after quadrature, 4 = after the first
+                              // kTq40J0 steps of solve_tq40_kernel (timing ablation only)
   int   debug_steps;          // CWBL_DEBUG_TQ_STEPS: > 0 runs only that many Householder steps
                               // in solve_tq_big_kernel (timing ablation only)
 };
@@ -208,7 +209,7 @@ hipError_t launch_assemble_record(hipStream_t s, int kp, const TreeDesc *trees, 
                                   SlabDev slab, long long g0, int npts, const int *nbr_cnt,
                                   const int *nbr_idx, int2 *info, double *ws);
 hipError_t launch_solve_tq40(hipStream_t s, int kp, SolveConsts c, SlabDev slab, long long g0,
-                             int npts, const double *ws, int2 *info);
+                             int npts, double *ws, int2 *info);
 
 // Split form of the KP = 128 slab path (configs[3]: k = 97..128).  solve_tq_big_kernel<128,
 // false, kBigJ0> assembles A and runs the first kBigJ0 Householder steps (4x4 register

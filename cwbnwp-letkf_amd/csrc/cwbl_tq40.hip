@@ -68,10 +68,13 @@ struct Tq40Smem {
   double tau[4][KP];
 };
 
-template <int KP>
+// STOP > 0: timing-ablation instantiations (CWBL_DEBUG_TQ_STOP = 4: after the first J0
+// steps, 2: after the tridiagonalisation, 3: after the quadrature; var is not written), so
+// that the production kernel's code is not perturbed by the early exits
+template <int KP, int STOP = 0>
 __global__ void __launch_bounds__(64, 2)
 solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
-                  const double *__restrict__ ws, int2 *__restrict__ info) {
+                  double *__restrict__ ws, int2 *__restrict__ info) {
   using HO = AsmRecord<KP>;
   constexpr int J0 = kTq40J0;         // steps with the prefix block (phase 1)
   constexpr int KT = KP - J0;         // slot rows J0 + l + 16 r
@@ -91,6 +94,12 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   // below 2^32 bytes)
   const unsigned wb = (unsigned)(valid ? gi : 0) * (unsigned)HO::WORDS;
   auto w = [&](int i) { return gld(ws, wb + (unsigned)i); };
+  // phase 1's reflectors are parked in the record's consumed A words between the end of
+  // phase 1 and the back-transform: column j of vector slot vs at word park(j, vs) + l
+  auto park = [](int j, int vs) { return 16 * (NV * j + vs); };
+  auto wst = [&](unsigned base, int i, double v) {
+    *reinterpret_cast<double *>(reinterpret_cast<char *>(ws) + (base + (unsigned)i) * 8u) = v;
+  };
   auto apk = [](int r, int col) {  // packed lower index of A(r, col)
     return col <= r ? r * (r + 1) / 2 + col : col * (col + 1) / 2 + r;
   };
@@ -297,12 +306,25 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       if constexpr (col < J0) Pb[col] = fma(-vP, wc, fma(-wP, vc, Pb[col]));
     });
   });
+  // park phase 1's reflectors (registers free for phase 2 and the quadrature)
+  sfor<J0>([&](auto jj) {
+    constexpr int j = decltype(jj)::value;
+    wst(wb, park(j, 0) + l, Pb[j]);
+    sfor<NS>([&](auto rr) { wst(wb, park(j, decltype(rr)::value + 1) + l, A[decltype(rr)::value][j]); });
+  });
+  // A (one-wave) workgroup barrier ends the scheduling region: without it the compiler
+  // schedules the whole straight-line phase 1 + phase 2 as one region and spills 2x as much
+  __syncthreads();
   // the prefix rows of Q^T b1, Q^T x' are final (later reflectors vanish there)
   if (pre) {
     sm.tq[q][l][2] = ubP;
     sm.tq[q][l][3] = uxP;
   }
 
+  if constexpr (STOP == 4) {  // timing ablation: phase 1 only
+    if (valid && l == 0) info[gi] = make_int2(ptot, (int)(trace + uxP + A[1][KP - 1]));
+    return;
+  }
   // ---- phase 2: steps J0 .. KP-3 on the trailing rows (solve_tq4_kernel's step) -----------
   // Steps j >= k - 2 (k < KP) are exact no-ops: the padding rows and columns of A are the
   // identity, so x = 0 there, tau = 0 and beta = A(j+1,j); running them keeps the code
@@ -410,6 +432,10 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   }
   __syncthreads();
 
+  if constexpr (STOP == 2) {  // timing ablation: tridiagonalisation only
+    if (valid && l == 0) info[gi] = make_int2(ptot, (int)(trace + ux[1]));
+    return;
+  }
   // ---- T^-1/2 u2 by quadrature, T^-1 u2 exactly --------------------------------------------
   // lambda^-1/2 = (2/pi) int_0^inf dt / (t^2 + lambda) with the elliptic substitution and
   // the midpoint rule on the spectrum bound [m, M] (solve_tq_kernel, cwbl_tq.hip): each node
@@ -483,8 +509,23 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     dpart = i < KP ? fma(u1, z[vs], dpart) : dpart;
   });
   const double d = row16_sum(dpart);
+  if constexpr (STOP == 3) {  // timing ablation: up to the quadrature
+    if (valid && l == 0) info[gi] = make_int2(ptot, (int)(d + ys[0] + ys[1] + ys[2]));
+    return;
+  }
 
   // ---- back-transform: y <- Q y = H_0 H_1 ... H_{KP-3} y ----------------------------------
+  double pv[J0][NV];  // phase 1's reflectors, loaded behind phase 2's
+  {
+    unsigned pbase = wb;
+    asm volatile("" : "+v"(pbase));  // opaque: the compiler must load, not forward the stores
+    sfor<J0>([&](auto jj) {
+      sfor<NV>([&](auto vv) {
+        constexpr int j = decltype(jj)::value, vs = decltype(vv)::value;
+        pv[j][vs] = gld(ws, pbase + (unsigned)(park(j, vs) + l));
+      });
+    });
+  }
   double y[NV];
   sfor<NV>([&](auto vv) { y[decltype(vv)::value] = ys[decltype(vv)::value]; });
   sfor<KT - 2>([&](auto jj) {  // phase 2's reflectors (rows > J0 only)
@@ -510,13 +551,13 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   sfor<J0>([&](auto jj) {  // phase 1's reflectors: prefix register j and slot column j
     constexpr int j = J0 - 1 - decltype(jj)::value, J1 = j + 1;
     const double tj = sm.tau[q][j];
-    const double v0 = !pre ? 0.0 : l == J1 ? 1.0 : Pb[j];  // Pb[j] is 0 at rows <= j + 1
+    const double v0 = !pre ? 0.0 : l == J1 ? 1.0 : pv[j][0];  // 0 at rows <= j + 1
     double vv[NS];
     double a = v0 * y[0];
     sfor<NS>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
-      if constexpr (J1 == J0 && r == 0) vv[r] = l == 0 ? 1.0 : A[r][j];
-      else vv[r] = A[r][j];
+      if constexpr (J1 == J0 && r == 0) vv[r] = l == 0 ? 1.0 : pv[j][r + 1];
+      else vv[r] = pv[j][r + 1];
       a = fma(vv[r], y[r + 1], a);
     });
     a = row16_sum(a);
@@ -582,11 +623,16 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
 }
 
 hipError_t launch_solve_tq40(hipStream_t s, int kp, SolveConsts c, SlabDev slab, long long g0,
-                             int npts, const double *ws, int2 *info) {
+                             int npts, double *ws, int2 *info) {
   if (npts <= 0) return hipSuccess;
   if (c.quad == nullptr || kp != kTq4KP) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP>), dim3((npts + 3) / 4), dim3(64), 0, s, c, slab,
-                     g0, npts, ws, info);
+  const dim3 grid((npts + 3) / 4);
+  switch (c.debug_stop) {
+    case 2: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 2>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); break;
+    case 3: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 3>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); break;
+    case 4: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 4>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); break;
+    default: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info);
+  }
   return hipGetLastError();
 }
 

@@ -9,5 +9,5 @@ for st in ${STOPS:-11 1 0}; do
   echo "stop=$st"; python3 -c "
 import csv,sys
 for r in csv.DictReader(open('$f')):
-    print('  %-45s calls %4s avg %.3f ms total %.1f ms' % (r['Name'].split('(')[0][:45], r['Calls'], float(r['AverageNs'])/1e6, float(r['TotalDurationNs'])/1e6))"
+    print('  %-45s calls %4s avg %.3f ms total %.1f ms' % (r['Name'].split('(')[0][-45:], r['Calls'], float(r['AverageNs'])/1e6, float(r['TotalDurationNs'])/1e6))"
 done
