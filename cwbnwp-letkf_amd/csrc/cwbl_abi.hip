@@ -349,7 +349,8 @@ SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps,
   c.r2 = search_r2();
   c.max_sweeps = 30;
   if (const char *e = std::getenv("CWBL_DEBUG_MAX_SWEEPS")) c.max_sweeps = std::atoi(e);
-  c.quad = S.quad.as<double2>();
+  c.quad_r = S.quad.as<double2>();
+  c.quad = c.quad_r ? c.quad_r + (size_t)2 * kQuadLevels * 32 : nullptr;  // 31 nodes
   if (const char *e = std::getenv("CWBL_DEBUG_TQ_STOP")) c.debug_stop = std::atoi(e);
   if (const char *e = std::getenv("CWBL_DEBUG_STAGGER")) c.stagger = std::atoi(e);
   if (const char *e = std::getenv("CWBL_DEBUG_TQ_STEPS")) c.debug_steps = std::atoi(e);
@@ -399,8 +400,10 @@ int cwbl_init(const cwbl_init_params *p) {
   HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.sstream, hipStreamNonBlocking));
   {
-    std::vector<double2> tab((size_t)kQuadLevels * 32);
-    for (int l = 1; l <= kQuadLevels; ++l) quad_table(l, &tab[(size_t)(l - 1) * 32]);
+    std::vector<double2> tab((size_t)3 * kQuadLevels * 32);  // 15, 23, 31 nodes
+    for (int r = 0; r < 3; ++r)
+      for (int l = 1; l <= kQuadLevels; ++l)
+        quad_table(l, &tab[((size_t)r * kQuadLevels + (l - 1)) * 32], 8 * (r + 2) - 1);
     HIPCHK(S.quad.ensure(tab.size() * sizeof(double2)));
     HIPCHK(hipMemcpy(S.quad.p, tab.data(), tab.size() * sizeof(double2), hipMemcpyHostToDevice));
   }

@@ -87,6 +87,8 @@ struct SolveConsts {
   float r2;                   // gc1999**2
   int   max_sweeps;           // Jacobi sweep cap (CWBL_DEBUG_MAX_SWEEPS overrides; ablation only)
   const double2 *quad;        // [kQuadLevels][32] (t2, w) of the x^-1/2 rule (solve_tq_kernel)
+  const double2 *quad_r;      // [3][kQuadLevels][32]: the rules of 15, 23, 31 nodes (= quad),
+                              // 8 R - 1 nodes for R = 2, 3, 4 rounds of solve_tq40_kernel
   int   stagger;              // CWBL_DEBUG_STAGGER: start-phase offset unit in cycles (experiment)
   int   debug_stop;           // CWBL_DEBUG_TQ_STOP: 1 = after assembly, 2 = after
                               // tridiagonalisation, 3 = after quadrature, 4 = after the first
@@ -99,7 +101,11 @@ struct SolveConsts {
 // covers spectra with max/min <= 10^L using kQuadNodes nodes (slot 31 of a level is unused).
 constexpr int kQuadNodes = 31;
 constexpr int kQuadLevels = 12;
-void quad_table(int level, double2 *out32);
+void quad_table(int level, double2 *out32, int nodes = kQuadNodes);
+// Rounds of 8 nodes (the last round's slot 7 is the exact T^-1 solve) solve_tq40_kernel runs
+// at a level: the (8 R - 1)-node rule is as accurate as the 31-node one there (relative error
+// <= 1e-15; tests/test_quadrature.py)
+__host__ __device__ constexpr int quad_rounds(int level) { return level <= 2 ? 2 : level == 3 ? 3 : 4; }
 
 // Point enumeration of a slab: g = i + ix_lim*(j + iy_lim*kz).
 struct SlabDev {

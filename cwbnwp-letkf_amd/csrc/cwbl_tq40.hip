@@ -449,6 +449,12 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     dec *= 10.0;
     ++level;
   }
+  // rounds of 8 nodes: the wave's largest need (quad_rounds) over its four points, with the
+  // (8 R - 1)-node rule of each point's own level; slot 7 of the last round is T^-1 u2
+  const int rp = quad_rounds(level);
+  const int R = __ballot(rp == 4) ? 4 : __ballot(rp == 3) ? 3 : 2;  // wave-uniform
+  const int NQ = 8 * R - 1;
+  const double2 *qtab = c.quad_r + ((size_t)(R - 2) * kQuadLevels + (level - 1)) * 32;
   const int side = l >> 3, n8 = l & 7;
   const double(*T)[4] = sm.tq[q];
   const double *tq0 = &T[side ? KP - 1 : 0][0];
@@ -456,11 +462,11 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   const int cs = side ? 5 : 1;  // coupling with the previous row of the walk
   double ys[NV], z[NV];
   sfor<NV>([&](auto vv) { ys[decltype(vv)::value] = 0.0; });
-  for (int round = 0; round < 4; ++round) {
+  for (int round = 0; round < R; ++round) {
     const int node = 8 * round + n8;
-    const double2 tw = c.quad[(level - 1) * 32 + min(node, kQuadNodes - 1)];
-    const double sigma = node < kQuadNodes ? m * tw.x : 0.0;
-    const double omega = node < kQuadNodes ? sqrt(m) * tw.y : 1.0;
+    const double2 tw = qtab[min(node, NQ - 1)];
+    const double sigma = node < NQ ? m * tw.x : 0.0;
+    const double omega = node < NQ ? sqrt(m) * tw.y : 1.0;
     double hh[H], mm[H];
     double dl = tq0[0] + sigma, gt = tq0[3];
     double rdl = rcp64(dl);
@@ -487,7 +493,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       sm.qx[q][row_of(t)][n8] = omega * xv;
     });
     __syncthreads();
-    const bool last = round == 3;  // node 31 (slot 7 of the last round) is T^-1 u2
+    const bool last = round == R - 1;  // slot 7 of the last round is T^-1 u2
     sfor<NV>([&](auto vv) {
       constexpr int vs = decltype(vv)::value;
       const int i = vrow(vs);
@@ -625,7 +631,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
 hipError_t launch_solve_tq40(hipStream_t s, int kp, SolveConsts c, SlabDev slab, long long g0,
                              int npts, double *ws, int2 *info) {
   if (npts <= 0) return hipSuccess;
-  if (c.quad == nullptr || kp != kTq4KP) return hipErrorInvalidValue;
+  if (c.quad_r == nullptr || kp != kTq4KP) return hipErrorInvalidValue;
   const dim3 grid((npts + 3) / 4);
   switch (c.debug_stop) {
     case 2: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 2>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); break;

@@ -7,7 +7,8 @@
 // geometrically (Hale, Higham & Trefethen, SIAM J. Numer. Anal. 46 (2008), method for
 // A^-1/2 on a real positive spectrum):
 //   x^-1/2 ~= sum_j w_j / (t2_j + x),  t2_j = sc^2(u_j),  w_j = (2/pi)(K/N) dn(u_j)/cn^2(u_j)
-// Level L covers kappa = 10^L.  Elliptic functions are evaluated in long double by the
+// Level L covers kappa = 10^L.  N = 31 nodes everywhere (kQuadNodes); solve_tq40_kernel also
+// uses N = 15 up to level 2 and N = 23 at level 3, which are as accurate there (<= 1e-15).  Elliptic functions are evaluated in long double by the
 // AGM / descending Landen scheme (Abramowitz & Stegun 16.4); nodes past K/2 use the
 // reflection u -> K - u (sc(K-v) = 1/(k' sc(v)), dn/cn^2 (K-v) = dn(v)/(k' sn^2(v))) so that
 // no quantity is formed from a cancelling cn.
@@ -61,12 +62,11 @@ long double ellipk(long double m) {
 
 }  // namespace
 
-void quad_table(int level, double2 *out) {
+void quad_table(int level, double2 *out, int N) {
   const long double kappa = powl(10.0L, (long double)level);
   const long double m = 1.0L - 1.0L / kappa;
   const long double kc = sqrtl(1.0L / kappa);  // k'
   const long double K = ellipk(m);
-  const int N = kQuadNodes;
   for (int j = 0; j < 32; ++j) {
     if (j >= N) {
       out[j] = make_double2(0.0, 0.0);
@@ -91,9 +91,14 @@ void quad_table(int level, double2 *out) {
 
 }  // namespace cwbl
 
-// Test hook (not part of the public header): the table of one level, 32 (t2, w) pairs.
-extern "C" int cwbl_debug_quad_table(int level, double *t2w) {
-  if (level < 1 || level > cwbl::kQuadLevels || !t2w) return 1;
-  cwbl::quad_table(level, reinterpret_cast<double2 *>(t2w));
+// Test hooks (not part of the public header): the table of one level, 32 (t2, w) pairs, for
+// the kQuadNodes-node rule and for an n-node rule (n <= 31; the short rules of
+// solve_tq40_kernel, quad_nodes_for_rounds).
+extern "C" int cwbl_debug_quad_table_n(int level, int n, double *t2w) {
+  if (level < 1 || level > cwbl::kQuadLevels || n < 1 || n > 31 || !t2w) return 1;
+  cwbl::quad_table(level, reinterpret_cast<double2 *>(t2w), n);
   return 0;
+}
+extern "C" int cwbl_debug_quad_table(int level, double *t2w) {
+  return cwbl_debug_quad_table_n(level, cwbl::kQuadNodes, t2w);
 }

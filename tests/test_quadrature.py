@@ -18,10 +18,14 @@ def lib():
     return abi.load_library()
 
 
-def table(lib, level):
+def table(lib, level, n=31):
     buf = np.zeros(64)
-    assert lib.cwbl_debug_quad_table(level, buf.ctypes.data_as(C.POINTER(C.c_double))) == 0
-    return buf.reshape(32, 2)[:31, 0], buf.reshape(32, 2)[:31, 1]
+    p = buf.ctypes.data_as(C.POINTER(C.c_double))
+    if n == 31:
+        assert lib.cwbl_debug_quad_table(level, p) == 0
+    else:
+        assert lib.cwbl_debug_quad_table_n(level, n, p) == 0
+    return buf.reshape(32, 2)[:n, 0], buf.reshape(32, 2)[:n, 1]
 
 
 # relative accuracy the kernel relies on, per decade of the spectrum
@@ -38,11 +42,25 @@ def test_rule_accuracy(lib, level):
     assert err <= BOUND[level], err
 
 
+# solve_tq40_kernel runs 8 R - 1 nodes (R = quad_rounds(level), cwbl_internal.h: 2 rounds up to
+# level 2, 3 at level 3, 4 above) with the exact T^-1 solve in the last slot; the short rules
+# must be as accurate there as the 31-node one
+@pytest.mark.parametrize("level,n", [(1, 15), (2, 15), (3, 23)])
+def test_short_rules_accuracy(lib, level, n):
+    t2, w = table(lib, level, n)
+    assert np.all(t2 > 0) and np.all(w > 0) and np.all(np.diff(t2) > 0)
+    lam = np.geomspace(1.0, 10.0 ** level, 20000)
+    approx = (w[None, :] / (t2[None, :] + lam[:, None])).sum(1)
+    err = np.max(np.abs(approx * np.sqrt(lam) - 1.0))
+    assert err <= 2e-15, err
+
+
 def test_bad_level_rejected(lib):
     buf = np.zeros(64)
     p = buf.ctypes.data_as(C.POINTER(C.c_double))
     assert lib.cwbl_debug_quad_table(0, p) != 0
     assert lib.cwbl_debug_quad_table(13, p) != 0
+    assert lib.cwbl_debug_quad_table_n(2, 32, p) != 0
 
 
 def test_matrix_function_on_spd_tridiagonal(lib):
