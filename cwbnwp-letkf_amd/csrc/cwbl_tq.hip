@@ -676,7 +676,7 @@ hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees,
 // to the record, packed lower, with inflat on the live diagonal and 1 on the padding's
 // (decoupled unit rows, as solve_tq_kernel's blocks); row KP of the product is b1 = Yb d.
 template <int KP>
-__global__ void __launch_bounds__(64, 4)
+__global__ void __launch_bounds__(64, 5)
 assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
                        long long g0, int npts, const int *__restrict__ nbr_cnt,
                        const int *__restrict__ nbr_idx, int2 *__restrict__ info,
