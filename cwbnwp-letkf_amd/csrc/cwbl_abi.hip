@@ -680,7 +680,8 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
       Bs = std::min<long long>(Bs, 1 << 19);
       const bool rec = S.tq4 != 8;  // AsmRecord + solve_tq40_kernel, else Tq4Handoff
-      HIPCHK(S.wsa.ensure((size_t)Bs * 8 *
+      // (+1: the spare record of solve_tq40_kernel's lanes past the batch)
+      HIPCHK(S.wsa.ensure((size_t)(Bs + 1) * 8 *
                           (rec ? AsmRecord<kTq4KP>::WORDS : Tq4Handoff<kTq4KP, kTq4J0>::WORDS)));
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
         const int ns = (int)std::min<long long>(Bs, nb - s0);

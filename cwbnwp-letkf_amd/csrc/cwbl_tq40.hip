@@ -91,8 +91,9 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   const int k = c.k;
   const int ptot = valid ? info[gi].x : 0;
   // record words of this point: SGPR base + 32-bit offset (the host keeps a batch's records
-  // below 2^32 bytes)
-  const unsigned wb = (unsigned)(valid ? gi : 0) * (unsigned)HO::WORDS;
+  // below 2^32 bytes).  A lane past the batch works on the spare record npts (the host
+  // allocates npts + 1): it parks into it, so it must not share a live point's record
+  const unsigned wb = (unsigned)(valid ? gi : npts) * (unsigned)HO::WORDS;
   auto w = [&](int i) { return gld(ws, wb + (unsigned)i); };
   // phase 1's reflectors are parked in the record's consumed A words between the end of
   // phase 1 and the back-transform: column j of vector slot vs at word park(j, vs) + l

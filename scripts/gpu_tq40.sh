@@ -2,7 +2,7 @@
 # KP = 40 split paths: parity test, then bench A/B (CWBL_TQ4 = 1 new record path, 8 old hand-off)
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "split_kp40 or c2_full or driver" > gpurun_out/pytest_tq40.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "split_kp40 or c2_full or driver or ragged" > gpurun_out/pytest_tq40.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_tq40.log
 [ $rc -eq 0 ] || { grep -E "^FAILED|^E  " gpurun_out/pytest_tq40.log | head -30; exit $rc; }
 for m in ${MODES:-1 8}; do

@@ -251,6 +251,43 @@ def test_split_kp40_path_vs_one_kernel_and_oracle(k, monkeypatch):
         assert rel <= INCR_TOL, (mode, rel)
 
 
+def test_split_kp40_ragged_record_batches(monkeypatch):
+    """Record sub-batches whose point count is not a multiple of four: the last wave of
+    solve_tq40_kernel has lanes past the batch, which must not disturb a live point's record
+    (they work on a spare record).  31x29x7 = 6293 points in sub-batches of 512 (the last has
+    149).  Every point against the oracle, and the same analysis as one record batch."""
+    import ctypes as C
+    from cwbl import synth
+    w = synth.make("c2", seed=11, nx=31, ny=29, nz=7, n_obs=240)
+    assert w.points % 4 == 1
+    out = {}
+    for sub in ("512", "0"):
+        monkeypatch.setenv("CWBL_TQ4_SUB", sub)
+        _cores.clear()
+        c = abi.Core(w.k, device=0)
+        c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+        var = w.var.copy()
+        st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+        c.finalize()
+        assert st.solved > 0 and st.nonconverged == 0
+        out[sub] = var
+    np.testing.assert_array_equal(out["512"].view(np.uint32), out["0"].view(np.uint32))
+    ref = w.var.copy()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(w.x, w.y, w.alt, ref)), 16,
+                                  C.byref(abi.Stats()))
+    assert rc == 0
+    rel = increment_rel_rms(out["512"], ref, w.var)
+    assert rel <= INCR_TOL, rel
+    # the first point of every sub-batch (whose record a lane past the batch would share)
+    # and the last point, individually
+    d = (out["512"] - ref).reshape(w.k, -1)
+    inc = (ref - w.var).reshape(w.k, -1)
+    for g in list(range(0, w.points, 512)) + [w.points - 1]:
+        assert np.sqrt((d[:, g] ** 2).sum()) <= 1e-5 * max(np.sqrt((inc[:, g] ** 2).sum()), 1e-6), g
+
+
 def test_c2_full_size_properties():
     """Full C2 size (300x300x50, k=40): properties that do not need the oracle everywhere,
     plus an oracle check on a column block."""
