@@ -102,6 +102,10 @@ struct State {
   DevBuf tdesc, nbr_cnt, nbr_idx, info, stats;
   DevBuf nbr_cnt2, nbr_idx2;                          // second list buffer (search overlap)
   hipStream_t sstream = nullptr;                      // neighbour searches of later batches
+  hipStream_t tstream = nullptr;                      // solve_tq40_kernel (record path)
+  bool tq40_streams = true;  // CWBL_TQ40_STREAMS=0: solve_tq40_kernel on S.stream (no overlap)
+  DevBuf wsa2, info2;                                 // second record / info buffers
+  std::vector<hipEvent_t> cevents;                    // record-path events (cevent)
   int lead_div = 0;                                   // first batch = npts / lead_div (0: off)
   bool serial_search = false;                         // CWBL_DEBUG_SERIAL=1: searches on S.stream
   // Points per search/solve batch.  Measured on C2 (one GPU, ms per variable): 40 k 113,
@@ -162,6 +166,17 @@ hipError_t stage(DevBuf &dst, const void *src, size_t bytes, int memory) {
                         memory == CWBL_MEM_DEVICE ? hipMemcpyDeviceToDevice
                                                   : hipMemcpyHostToDevice,
                         S.stream);
+}
+
+hipError_t cevent(int i, hipEvent_t *out) {  // events of the record path (timing off)
+  while ((int)S.cevents.size() <= i) {
+    hipEvent_t e;
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (r != hipSuccess) return r;
+    S.cevents.push_back(e);
+  }
+  *out = S.cevents[i];
+  return hipSuccess;
 }
 
 hipError_t event(int i, hipEvent_t *out) {
@@ -322,6 +337,11 @@ void release_obs() {
 
 void release_all() {
   release_obs();
+  for (DevBuf *b : {&S.wsa2, &S.info2}) b->release();
+  for (hipEvent_t e : S.cevents) (void)hipEventDestroy(e);
+  S.cevents.clear();
+  if (S.tstream) (void)hipStreamDestroy(S.tstream);
+  S.tstream = nullptr;
   for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.nbr_cnt2, &S.nbr_idx2, &S.info, &S.stats, &S.sx,
                     &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev,
                     &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad, &S.wsa, &S.flags})
@@ -399,6 +419,7 @@ int cwbl_init(const cwbl_init_params *p) {
   S.ws_bytes = p->workspace_bytes ? p->workspace_bytes : (size_t(2) << 30);
   HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.sstream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&S.tstream, hipStreamNonBlocking));
   {
     std::vector<double2> tab((size_t)3 * kQuadLevels * 32);  // 15, 23, 31 nodes
     for (int r = 0; r < 3; ++r)
@@ -412,6 +433,8 @@ int cwbl_init(const cwbl_init_params *p) {
   S.tq4 = 1;
   if (const char *e = std::getenv("CWBL_TQ4")) S.tq4 = std::atoi(e);
   if (const char *e = std::getenv("CWBL_TQ4_SUB")) S.tq4_sub = std::atoll(e);
+  S.tq40_streams = true;
+  if (const char *e = std::getenv("CWBL_TQ40_STREAMS")) S.tq40_streams = std::atoi(e) != 0;
   S.big_split = true;
   S.big_sub = 32768;
   {
@@ -618,6 +641,17 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   int ev = 4;
   std::vector<std::pair<int, int>> search_ev, solve_ev;
   std::vector<int> done_ev;
+  // Record path with the solves on their own stream (S.tstream): solve_tq40_kernel of a
+  // record batch overlaps the assembly of the next one (the assembly keeps the matrix pipe
+  // busy, the four-point solve is latency-bound).  Two record and two info buffers; an
+  // assembly waits for the solve two record batches back (record reuse) and for the info
+  // reduction two search batches back (info reuse).
+  const bool conc = S.tq40_streams && S.tq4 && S.tq4 != 8 && S.kp == kTq4KP && !S.jacobi;
+  int nrec = 0;                 // record batches so far
+  std::vector<int> rec_done;    // cevent after each record batch's solve (on S.tstream)
+  std::vector<int> info_done;   // cevent after each search batch's info reduction
+  int cev = 0;
+  if (conc) HIPCHK(S.info2.ensure((size_t)B * sizeof(int2)));
   for (long long bi = 0; bi < nbat; ++bi) {
     const long long g0 = plan[bi].first;
     const int nb = plan[bi].second;
@@ -681,11 +715,33 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       Bs = std::min<long long>(Bs, 1 << 19);
       const bool rec = S.tq4 != 8;  // AsmRecord + solve_tq40_kernel, else Tq4Handoff
       // (+1: the spare record of solve_tq40_kernel's lanes past the batch)
-      HIPCHK(S.wsa.ensure((size_t)(Bs + 1) * 8 *
-                          (rec ? AsmRecord<kTq4KP>::WORDS : Tq4Handoff<kTq4KP, kTq4J0>::WORDS)));
+      const size_t wbytes = (size_t)(Bs + 1) * 8 *
+                            (rec ? AsmRecord<kTq4KP>::WORDS : Tq4Handoff<kTq4KP, kTq4J0>::WORDS);
+      HIPCHK(S.wsa.ensure(wbytes));
+      if (conc) HIPCHK(S.wsa2.ensure(wbytes));
+      int2 *binfo = conc && (bi & 1) ? S.info2.as<int2>() : S.info.as<int2>();
+      if (conc && bi >= 2)  // this search batch's info buffer: reduced two batches back
+        HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[info_done[bi - 2]], 0));
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
         const int ns = (int)std::min<long long>(Bs, nb - s0);
-        if (rec) {
+        if (conc) {
+          double *recp = (nrec & 1) ? S.wsa2.as<double>() : S.wsa.as<double>();
+          if (nrec >= 2)  // this record buffer: solved two record batches back
+            HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[rec_done[nrec - 2]], 0));
+          HIPCHK(launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
+                                        ncnt + s0 * nt, nidx + s0 * list_cap, binfo + s0,
+                                        recp));
+          hipEvent_t ea, et;
+          HIPCHK(cevent(cev, &ea));
+          HIPCHK(cevent(cev + 1, &et));
+          HIPCHK(hipEventRecord(ea, S.stream));
+          HIPCHK(hipStreamWaitEvent(S.tstream, ea, 0));
+          HIPCHK(launch_solve_tq40(S.tstream, S.kp, c, sd, g0 + s0, ns, recp, binfo + s0));
+          HIPCHK(hipEventRecord(et, S.tstream));
+          rec_done.push_back(cev + 1);
+          cev += 2;
+          ++nrec;
+        } else if (rec) {
           HIPCHK(launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
                                         ncnt + s0 * nt, nidx + s0 * list_cap,
                                         S.info.as<int2>() + s0, S.wsa.as<double>()));
@@ -703,14 +759,26 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
                              nullptr, nullptr, nullptr, nullptr, nullptr,
                              S.info.as<int2>()));
-    HIPCHK(hipEventRecord(cc, S.stream));
     HIPCHK(hipEventRecord(dn, S.stream));  // this batch's lists are free again
-    HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), nb, dst));
+    if (conc) {  // the solves and the info reduction of this batch on S.tstream
+      int2 *binfo = (bi & 1) ? S.info2.as<int2>() : S.info.as<int2>();
+      HIPCHK(launch_reduce_info(S.tstream, binfo, nb, dst));
+      HIPCHK(hipEventRecord(cc, S.tstream));
+      hipEvent_t ir;
+      HIPCHK(cevent(cev, &ir));
+      HIPCHK(hipEventRecord(ir, S.tstream));
+      info_done.push_back(cev++);
+    } else {
+      HIPCHK(hipEventRecord(cc, S.stream));
+      HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), nb, dst));
+    }
     search_ev.push_back({ev, ev + 1});
     solve_ev.push_back({ev + 2, ev + 3});
     done_ev.push_back(ev + 4);
     ev += 5;
   }
+  if (conc && !info_done.empty())  // everything below follows the last solve and reduction
+    HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[info_done.back()], 0));
   if (vp->tune_q) {  // letkf_driver's Q species post-step (:253-278), on the resident slab
     hipEvent_t a, b;
     HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b));
@@ -738,7 +806,16 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   st.max_sweeps = (int)ds.max_sweeps;
   st.ms_prep = elapsed(0, 1);
   for (auto &p : search_ev) st.ms_search += elapsed(p.first, p.second);
-  for (auto &p : solve_ev) st.ms_solve += elapsed(p.first, p.second);
+  if (conc && !solve_ev.empty()) {
+    // the batches' solves overlap (assembly b + 1 with solve b): their span, not their sum
+    // (tune_q's pair, if any, is the last entry and follows the span)
+    const size_t nsv = (size_t)nbat;
+    st.ms_solve = elapsed(solve_ev[0].first, solve_ev[nsv - 1].second);
+    for (size_t i = nsv; i < solve_ev.size(); ++i)
+      st.ms_solve += elapsed(solve_ev[i].first, solve_ev[i].second);
+  } else {
+    for (auto &p : solve_ev) st.ms_solve += elapsed(p.first, p.second);
+  }
   st.ms_copy = elapsed(1, 2) + (sl->memory != CWBL_MEM_DEVICE ? elapsed(ev - 1, ev) : 0.0f);
   st.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
   if (stats) *stats = st;
