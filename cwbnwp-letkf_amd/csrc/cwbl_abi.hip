@@ -114,6 +114,7 @@ struct State {
   // batches keep each batch's lists and hand-off records nearer the caches and overlap
   // more of the search; below ~70 k the per-batch fixed costs win.
   long long max_batch = 160000;
+  bool max_batch_set = false;                         // CWBL_MAX_BATCH given: no ~6-batch rule
   DevBuf sx, sy, salt, svar;                          // slab staging (host-memory calls)
   DevBuf bcol, byo, byb, bxb, bxa, bev;               // solve_batch staging
   DevBuf qxyz, qnf, qidx, qr2;                        // search staging
@@ -446,7 +447,12 @@ int cwbl_init(const cwbl_init_params *p) {
   if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
   S.serial_search = false;
   if (const char *e = std::getenv("CWBL_DEBUG_SERIAL")) S.serial_search = std::atoi(e) != 0;
-  if (const char *e = std::getenv("CWBL_MAX_BATCH")) S.max_batch = std::max(256LL, std::atoll(e));
+  S.max_batch = 160000;
+  S.max_batch_set = false;
+  if (const char *e = std::getenv("CWBL_MAX_BATCH")) {
+    S.max_batch = std::max(256LL, std::atoll(e));
+    S.max_batch_set = true;  // an explicit cap is used as given
+  }
   S.inited = true;
   return CWBL_OK;
 }
@@ -588,6 +594,10 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   const size_t per_pt = (size_t)list_cap * 4 + (size_t)nt * 4 + 8;
   long long B = (long long)(S.ws_bytes / per_pt);
   B = std::min<long long>(B, S.max_batch);
+  // at least ~6 batches while they stay above 64 k points: with few batches the first search
+  // and the last solve run alone (an 8-GPU rank's C2 share, 562 k points: 12.8 ms per step
+  // in batches of 141 k, 12.3 in batches of 94 k; the full grid is indifferent in 100-160 k)
+  if (!S.max_batch_set) B = std::min<long long>(B, std::max<long long>(npts / 6, 64000));
   B = std::max<long long>(std::min<long long>(B, npts), 256);
   B = std::min<long long>(B, 1 << 22);
   // Batch plan: the first batch's search cannot overlap a solve, so it is short (a lead of
