@@ -332,6 +332,8 @@ def main():
         flops = synth.flops_total(k, solved, nobs_sum)
         achieved = flops / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else 0.0
         kp = ((k + 7) // 8) * 8 if k <= 64 else (96 if k <= 96 else 128)
+        if kp == 32 and not jacobi and os.environ.get("CWBL_TQ4", "1") != "0":
+            kp = 40  # k = 25..32 run the KP = 40 record path (cwbl_init)
         tq4 = os.environ.get("CWBL_TQ4", "1")
         split = not jacobi and kp == 40 and tq4 != "0"
         split128 = kp == 128 and k > 66 and os.environ.get("CWBL_BIG_SPLIT", "1") != "0"

@@ -447,6 +447,10 @@ int cwbl_init(const cwbl_init_params *p) {
   if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
   S.serial_search = false;
   if (const char *e = std::getenv("CWBL_DEBUG_SERIAL")) S.serial_search = std::atoi(e) != 0;
+  // k = 25..32: the KP = 40 record path (assembly + four-point solve; the padding rows are
+  // the identity and the steps past k - 2 exact no-ops) beats the one-wavefront KP = 32 solve
+  // (C2 grid: 91.6 against 134 ms per variable at k = 32)
+  if (S.kp == 32 && S.tq4 && !S.jacobi) S.kp = kTq4KP;
   S.max_batch = 160000;
   S.max_batch_set = false;
   if (const char *e = std::getenv("CWBL_MAX_BATCH")) {
