@@ -314,9 +314,13 @@ __device__ __forceinline__ int stage_columns(
         const int jn = divn(q), v = q - jn * nvar;
         const int slot = slot_next;
         const int col = slot * nvar + v;
-        // the next chunk's slot first: it depends on nothing gathered below
+        // the next chunk's slot first: it depends on nothing gathered below.  The load is
+        // unconditional (a lane past the list, or every lane on the last chunk, reads the
+        // slot of pair npairs - 1: a valid table index whose column w = 0 zeroes): behind a
+        // branch, the skipping path left the wait for the gathers' operands at vmcnt(0), so
+        // the gathers waited a whole round trip for this prefetch.
         const int nb = base + CHUNK;
-        if (sl < min(CHUNK, npairs - nb)) slot_next = gld(lst, list_slot(divn(nb + sl)));
+        slot_next = gld(lst, list_slot(divn(min(nb + sl, npairs - 1))));
         // Gathers without a branch: a lane past nsl keeps the slot of an earlier chunk (or
         // 0), a valid table index, and its column is zeroed by w = 0 below.  The bg row part
         // goes first and as 16-B loads (b0 is a multiple of 4 floats: KP % 8 == 0), then
