@@ -337,7 +337,7 @@ def main():
         tq4 = os.environ.get("CWBL_TQ4", "1")
         split = not jacobi and kp == 40 and tq4 != "0"
         split128 = kp == 128 and k > 66 and os.environ.get("CWBL_BIG_SPLIT", "1") != "0"
-        kpair = (("assemble_record_kernel<40, 5>", "solve_tq40_kernel<40, 0>") if tq4 != "8" else
+        kpair = (("assemble_record_kernel<40, 4>", "solve_tq40_kernel<40, 0>") if tq4 != "8" else
                  ("solve_tq_kernel<40, false, 8>", "solve_tq4_kernel<40, 8>"))
         kname = (" + ".join(kpair) if split else
                  "solve_tq_big_kernel<128, false, 64> + solve_tqb_tail_kernel<128, 64, 2>"

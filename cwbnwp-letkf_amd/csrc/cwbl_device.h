@@ -401,6 +401,127 @@ __device__ __forceinline__ int stage_columns(
   return ptot;
 }
 
+// Analysis-path staging for the one-wavefront matrix-core assembly: two chunks per round
+// (stage_columns_pair) or one (stage_columns); build with -DCWBL_STAGE_PAIR=0 for the latter.
+#ifndef CWBL_STAGE_PAIR
+#define CWBL_STAGE_PAIR 1
+#endif
+constexpr bool kStagePair = CWBL_STAGE_PAIR != 0;
+
+// The value of lane i ^ 32 (the other half wave), by one v_permlane32_swap.
+__device__ __forceinline__ int other_half(int x, int half) {
+  const auto s = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return half ? s[0] : s[1];  // s[0]: lanes 32-63 get x[i-32]; s[1]: lanes 0-31 get x[i+32]
+}
+__device__ __forceinline__ float other_half(float x, int half) {
+  return __int_as_float(other_half(__float_as_int(x), half));
+}
+
+// stage_columns for one wavefront, CHUNK = 32, analysis path, two chunks per round: the
+// weight of a column is computed once, not by both lanes that stage its bg row.  Lane
+// (half, sl) owns column sl of chunk c + half (its slot, QC flag, error, omm, coordinates,
+// weight) and stages half `half` of the bg row of column sl of chunk c, then of chunk c + 1;
+// the weight of the column it stages but does not own comes from lane sl + 32 (half 0) or
+// sl (half 1) by one swap.  Same columns, order and arithmetic as stage_columns.
+template <int KP, int CHUNK, int PITCH, class Acc>
+__device__ __forceinline__ int stage_columns_pair(
+    ColumnChunk<KP, CHUNK, float, PITCH> &ch, const TreeDesc *__restrict__ trees,
+    const SolveConsts &c, int gi, int lane, const int *__restrict__ nbr_cnt,
+    const int *__restrict__ nbr_idx, const float3 pt, Acc &&accumulate) {
+  static_assert(CHUNK == 32, "two lanes per staged column");
+  constexpr int VH = KP / 4;  // float2 of the bg row per lane
+  static_assert(KP % 8 == 0, "bg row split into 16-B loads");
+  int ptot = 0;
+  if (lane < 32) ch.expt[lane] = kExpT[lane];
+  if constexpr (PITCH > KP + 1) {
+    constexpr int NZ = PITCH - KP - 1;
+    for (int e = lane; e < CHUNK * NZ; e += 64) ch.yb[e / NZ][KP + 1 + e % NZ] = 0.0f;
+  }
+  const int sl = lane % CHUNK, half = lane / CHUNK;
+  for (int t = 0; t < c.ntrees; ++t) {
+    const TreeDesc T = trees[t];
+    const float q0 = pt.x * T.hclr_inv, q1 = pt.y * T.hclr_inv;  // get_lz (:243-253)
+    const float q2 = T.query3d ? pt.z * T.vclr_inv : 0.0f;
+    const int cnt = gptr(nbr_cnt)[(long long)gi * c.ntrees + t];
+    const int nvar = T.nvar;
+    const int npairs = cnt * nvar;
+    if (npairs == 0) continue;
+    const int *__restrict__ lst = nbr_idx + list_index(gi, c.list_cap, T.list_off);
+    const float rnv = 1.0f / (float)nvar;
+    auto divn = [&](int q) {
+      if (nvar == 1) return q;
+      int j = (int)((float)q * rnv);
+      j -= j * nvar > q ? 1 : 0;
+      j += (j + 1) * nvar <= q ? 1 : 0;
+      return j;
+    };
+    // a lane past the list reads the slot of pair npairs - 1 (a valid table index; the
+    // column's weight is 0)
+    auto slot_at = [&](int q) { return gld(lst, list_slot(divn(min(q, npairs - 1)))); };
+    auto var_of = [&](int q) { return q - divn(q) * nvar; };
+    auto gather_bg = [&](int col, f32x4 (&g)[VH / 2]) {
+      const unsigned b0 = (unsigned)(col * KP + 2 * VH * half);
+#pragma unroll
+      for (int i = 0; i < VH / 2; ++i) g[i] = gld4(T.col_bg, b0 + 4u * i);
+    };
+    auto put = [&](const f32x4 (&g)[VH / 2], float w) {  // bg * error_inv (:452)
+      float *d = &ch.yb[sl][2 * VH * half];
+#pragma unroll
+      for (int i = 0; i < VH / 2; ++i) {
+        *reinterpret_cast<float2 *>(d + 4 * i) = make_float2(g[i].x * w, g[i].y * w);
+        *reinterpret_cast<float2 *>(d + 4 * i + 2) = make_float2(g[i].z * w, g[i].w * w);
+      }
+    };
+    int slot_next = slot_at(half * CHUNK + sl);
+    for (int base = 0; base < npairs; base += 2 * CHUNK) {
+      const int qo = base + half * CHUNK + sl;  // the owned column's pair index
+      const int slot = slot_next;
+      slot_next = slot_at(qo + 2 * CHUNK);      // the next round's, behind nothing
+      const int slot_x = other_half(slot, half);
+      const int qa = base + sl, qb = qa + CHUNK;  // the staged columns of chunks c, c + 1
+      const int col_o = slot * nvar + var_of(qo);
+      const int col_a = (half ? slot_x : slot) * nvar + var_of(qa);
+      f32x4 g[VH / 2];
+      gather_bg(col_a, g);
+      const uint8_t okb = gld(T.col_ok, (unsigned)col_o);
+      const float err = gld(T.col_err, (unsigned)col_o);
+      const float omm = gld(T.col_omm, (unsigned)col_o);
+      const f32x4 rd = gld4(reinterpret_cast<const float *>(T.rdata), 4u * (unsigned)slot);
+      const bool ok = qo < npairs && okb != 0;
+      const float wv =
+          error_inv(c.weight_function, err, slot_r2(rd, T.tree_dim, q0, q1, q2), ch.expt);
+      const float w = ok ? wv : 0.0f;
+      const float yo = ok ? omm * wv : 0.0f;  // omm * error_inv (:451)
+      ptot += __popcll(__ballot(ok));
+      const float w_x = other_half(w, half);
+      // chunk c + 1's staged column and weight, formed now: four values (col_b, w_b, yo,
+      // slot_next) stay live across chunk c's accumulation
+      const int col_b = (half ? slot : slot_x) * nvar + var_of(qb);
+      const float w_b = half ? w : w_x;
+      if (half == 0) {
+        ch.yo[sl] = yo;
+        if constexpr (PITCH > KP) ch.yb[sl][KP] = yo;
+      }
+      put(g, half ? w_x : w);
+      __syncthreads();
+      accumulate(min(CHUNK, npairs - base));
+      __syncthreads();
+      if (base + CHUNK < npairs) {  // wave-uniform
+        gather_bg(col_b, g);
+        if (half == 1) {
+          ch.yo[sl] = yo;
+          if constexpr (PITCH > KP) ch.yb[sl][KP] = yo;
+        }
+        put(g, w_b);
+        __syncthreads();
+        accumulate(min(CHUNK, npairs - base - CHUNK));
+        __syncthreads();
+      }
+    }
+  }
+  return ptot;
+}
+
 // stage_columns for the 256-thread kernels (analysis path) with two chunk buffers: the
 // gathers of chunk c + 1 are issued before chunk c is accumulated and committed (weights,
 // LDS writes) to the other buffer after it, so their latency hides behind the matrix cores;
@@ -597,8 +718,15 @@ __device__ __forceinline__ void assemble_point_mfma(
   for (int t = 0; t < L::NTL; ++t) tile[t] = f64x4{0.0, 0.0, 0.0, 0.0};
   b1acc = 0.0;
   const int kk = lane >> 4, m = lane & 15;
-  ptot = stage_columns<KP, CHUNK, ASSEMBLED>(
-      ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in, [&](int nsl) {
+  auto stage = [&](auto &&acc) {
+    if constexpr (!ASSEMBLED && CHUNK == 32 && kStagePair)
+      return stage_columns_pair<KP, CHUNK, MfmaLayout<KP>::PITCH>(ch, trees, c, gi, lane, nbr_cnt,
+                                                                  nbr_idx, pt, acc);
+    else
+      return stage_columns<KP, CHUNK, ASSEMBLED>(ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt,
+                                                 col_off, yo_in, yb_in, acc);
+  };
+  ptot = stage([&](int nsl) {
         // Column s = 4 g + kk of the chunk feeds k-slot kk of group g; every staged column
         // past nsl is zero (stage_columns writes the whole chunk), and with YO_ROW the
         // staged rows are [Yb; yo; 0] up to 16 NT, so the operand reads need no predicate.

@@ -675,6 +675,10 @@ hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees,
 // straight from their C/D registers (row = 16 I + (lane >> 4) + 4 r, col = 16 J + (lane & 15))
 // to the record, packed lower, with inflat on the live diagonal and 1 on the padding's
 // (decoupled unit rows, as solve_tq_kernel's blocks); row KP of the product is b1 = Yb d.
+#ifndef CWBL_RECORD_WAVES
+#define CWBL_RECORD_WAVES 4
+#endif
+constexpr int kRecordWaves = CWBL_RECORD_WAVES;
 template <int KP, int WAVES = 5>
 __global__ void __launch_bounds__(64, WAVES)
 assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
@@ -732,7 +736,7 @@ hipError_t launch_assemble_record(hipStream_t s, int kp, const TreeDesc *trees, 
   if (npts <= 0) return hipSuccess;
   if (kp != kTq4KP) return hipErrorInvalidValue;
   // 5 waves per SIMD (96 VGPRs, 7 spilled): 0.7% faster per C2 step than 4 (110 VGPRs)
-  hipLaunchKernelGGL((assemble_record_kernel<kTq4KP>), dim3(npts), dim3(64), 0, s, trees, c,
+  hipLaunchKernelGGL((assemble_record_kernel<kTq4KP, kRecordWaves>), dim3(npts), dim3(64), 0, s, trees, c,
                      slab, g0, npts, nbr_cnt, nbr_idx, info, ws);
   return hipGetLastError();
 }
