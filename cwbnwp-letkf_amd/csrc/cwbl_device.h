@@ -407,6 +407,10 @@ __device__ __forceinline__ int stage_columns(
 #define CWBL_STAGE_PAIR 1
 #endif
 constexpr bool kStagePair = CWBL_STAGE_PAIR != 0;
+#ifndef CWBL_PAIR_PIPE
+#define CWBL_PAIR_PIPE 0
+#endif
+constexpr bool kPairPipe = CWBL_PAIR_PIPE != 0;
 
 // The value of lane i ^ 32 (the other half wave), by one v_permlane32_swap.
 __device__ __forceinline__ int other_half(int x, int half) {
@@ -503,11 +507,15 @@ __device__ __forceinline__ int stage_columns_pair(
         if constexpr (PITCH > KP) ch.yb[sl][KP] = yo;
       }
       put(g, half ? w_x : w);
+      const bool two = base + CHUNK < npairs;  // wave-uniform
+      if constexpr (kPairPipe) {  // chunk c + 1's bg rows in flight during chunk c's MFMAs
+        if (two) gather_bg(col_b, g);
+      }
       __syncthreads();
       accumulate(min(CHUNK, npairs - base));
       __syncthreads();
-      if (base + CHUNK < npairs) {  // wave-uniform
-        gather_bg(col_b, g);
+      if (two) {
+        if constexpr (!kPairPipe) gather_bg(col_b, g);
         if (half == 1) {
           ch.yo[sl] = yo;
           if constexpr (PITCH > KP) ch.yb[sl][KP] = yo;
