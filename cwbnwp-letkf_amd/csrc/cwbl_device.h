@@ -408,7 +408,7 @@ __device__ __forceinline__ int stage_columns(
 #endif
 constexpr bool kStagePair = CWBL_STAGE_PAIR != 0;
 #ifndef CWBL_PAIR_PIPE
-#define CWBL_PAIR_PIPE 0
+#define CWBL_PAIR_PIPE 1
 #endif
 constexpr bool kPairPipe = CWBL_PAIR_PIPE != 0;
 
