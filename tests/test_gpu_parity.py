@@ -252,6 +252,37 @@ def test_split_kp40_path_vs_one_kernel_and_oracle(k, monkeypatch):
         assert rel <= INCR_TOL, (mode, rel)
 
 
+@pytest.mark.parametrize("n_obs", [40, 120])
+def test_two_chunk_staging_at_sparse_densities(n_obs):
+    """The record kernel stages two 32-column chunks per round (stage_columns_pair: lane
+    (half, s) owns column s of chunk c + half and hands its slot and weight to the other half
+    wave).  Sparse obs sets put the points' candidate counts all over 0..~150, so rounds with
+    only chunk c, a partial chunk c + 1, exactly 32/64 candidates and empty lists all occur.
+    Every point against the oracle."""
+    import ctypes as C
+    from cwbl import synth
+    w = synth.make("c2", seed=11, nx=30, ny=30, n_obs=n_obs)
+    c = core(w.k)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    var = w.var.copy()
+    st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+    ref = w.var.copy()
+    ost = abi.Stats()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(w.x, w.y, w.alt, ref)), 16, C.byref(ost))
+    assert rc == 0
+    assert st.solved == ost.solved and st.nobs_sum == ost.nobs_sum
+    assert st.solved > 0
+    assert 10 < st.nobs_sum / st.solved < 100, st.nobs_sum / st.solved  # mean p: ~20, ~60
+    assert increment_rel_rms(var, ref, w.var) <= INCR_TOL
+    d = (var - ref).reshape(w.k, -1)
+    inc = (ref - w.var).reshape(w.k, -1)
+    dn = np.sqrt((d ** 2).sum(axis=0))
+    tol = 1e-5 * np.maximum(np.sqrt((inc ** 2).sum(axis=0)), 1e-6)
+    assert (dn <= tol).all(), int(np.argmax(dn - tol))
+
+
 def test_split_kp40_ragged_record_batches(monkeypatch):
     """Record sub-batches whose point count is not a multiple of four: the last wave of
     solve_tq40_kernel has lanes past the batch, which must not disturb a live point's record
