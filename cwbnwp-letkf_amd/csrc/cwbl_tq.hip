@@ -695,10 +695,12 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   float3 pt;
   slab_point(slab, g0 + gi, pt.x, pt.y, pt.z);
   f64x4 tile[L::NTL];
+  double dg[L::NT][3];
   double b1acc;
   int ptot;
-  assemble_point_mfma<KP, kTqChunk, false>(ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt,
-                                           nullptr, nullptr, nullptr, tile, b1acc, ptot);
+  assemble_point_mfma<KP, kTqChunk, false, kDiag4>(ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt,
+                                                   nullptr, nullptr, nullptr, tile, b1acc, ptot,
+                                                   dg);
   if (lane == 0) info[gi] = make_int2(ptot, 0);  // p = 0: the solve leaves var unchanged
   if (ptot == 0) return;
   if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the record
@@ -711,11 +713,32 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   const int k = c.k;
   const double inflat = (double)c.inflat;
   double *__restrict__ w = ws + (long long)gi * HO::WORDS;
+  auto put = [&](int row, int col, double a) {  // packed lower; inflat on the live diagonal
+    w[HO::TA + row * (row + 1) / 2 + col] = row != col ? a : row < k ? a + inflat : 1.0;
+  };
+  if constexpr (kDiag4) {
+    // dg[I][s], result lane 16i + 4b + j: C(16I + 4b + i, 16I + 4bc + j), bc = (b -/+ s) & 3
+    const int i = lane >> 4, b = (lane >> 2) & 3, j = lane & 3;
+#pragma unroll
+    for (int I = 0; I + 1 < L::NT; ++I) {
+      const int r0 = 16 * I + 4 * b + i;
+      if (i >= j) put(r0, 16 * I + 4 * b + j, dg[I][0]);
+#pragma unroll
+      for (int sh = 1; sh <= 2; ++sh) {
+        const int bc = (kRorDown ? b - sh : b + sh) & 3;
+        const double a = dg[I][sh];
+        if (bc < b) put(r0, 16 * I + 4 * bc + j, a);                           // lower block
+        else if (sh == 1) put(16 * I + 4 * bc + j, 16 * I + 4 * b + i, a);     // (b, b+-1)^T
+        // sh == 2, bc > b: the transpose of a lower block written by its other lane
+      }
+    }
+  }
   int t = 0;
 #pragma unroll
   for (int I = 0; I < L::NT; ++I)
 #pragma unroll
     for (int J = 0; J <= I; ++J, ++t) {
+      if (kDiag4 && I == J && I + 1 < L::NT) continue;  // written from dg above
       const int col = 16 * J + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
