@@ -245,6 +245,119 @@ def time_cycle(core, w, world, dev, x, y, alt):
                     "species; analysis only (no member<->column transposes, no file I/O)"}
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def _max_over_ranks(vals, world, dev, op=None):
+    if world == 1:
+        return vals
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op or dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
+
+
+def time_config(name, rank, world, local, dev, steps, warmup):
+    """One of BASELINE.json's other configurations timed like the headline one (detail only):
+    this rank's columns of the configuration's grid in HBM, the obs set broadcast once (RCCL
+    at N > 1), `warmup` + `steps` cwbl_analyze_var calls, max over ranks.  configs[3] (C4,
+    k = 128) and configs[4] (C5, dense radar on 600 x 600 x 60)."""
+    w = synth.make(name, shard=(rank, world) if world > 1 else None, local_noise=True)
+    types = [dict(family=1, type_id=w.radar_type, xyz=w.obs_xyz, obs=w.obs, hdxb=w.hdxb)]
+    if world > 1:
+        _, types = cdist.broadcast_obs_set(types if rank == 0 else None, w.k, dev, src=0)
+    else:
+        _, types = cdist.unpack_obs_set(torch.from_numpy(cdist.pack_obs_set(types, w.k)).to(dev))
+    x, y, alt, var = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt, w.var))
+    del w.var
+    core = abi.Core(w.k, device=local)
+    core.set_obs(cdist.builder_from(types, abi.MEM_DEVICE).build())
+    slab = abi.make_slab(x, y, alt, var, memory=abi.MEM_DEVICE)
+    for _ in range(warmup):
+        core.analyze_var(w.vp, slab)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    stats = [core.analyze_var(w.vp, slab) for _ in range(steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    solved = sum(s.solved for s in stats)
+    nobs = sum(s.nobs_sum for s in stats)
+    ms_solve = sum(s.ms_solve for s in stats)
+    flops = synth.flops_total(w.k, solved, nobs)
+    el, pts, sol, nsum = _max_over_ranks([el], world, dev) + _max_over_ranks(
+        [float(sum(s.points for s in stats)), float(solved), float(nobs)], world, dev,
+        dist.ReduceOp.SUM if world > 1 else None)
+    core.finalize()
+    cfg = w.extra["cfg"]
+    tf = flops / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else 0.0
+    return {"workload": f"{name}: {cfg['nx']}x{cfg['ny']}x{cfg['nz']} grid, k={w.k}, "
+                        f"{cfg['n_obs']} obs (hclr {cfg['hclr']} km, vclr {cfg['vclr']} km), "
+                        f"max_lz_pts {cfg['max_lz']}",
+            "value": pts / el, "unit": "grid-points/s", "ms_per_step": el / steps * 1e3,
+            "steps": steps, "warmup": warmup, "n_gpus": world,
+            "mean_p": nsum / max(sol, 1),
+            "nonconverged": sum(s.nonconverged for s in stats),
+            "rank0_solve_tflops_F": tf, "rank0_frac_F": tf / FP64_PEAK_TFLOPS}
+
+
+def time_host_memory(w, local, steps, warmup, pinned):
+    """The headline configuration with the slab in HOST memory (MEM_HOST): every call copies
+    x, y, alt and the 720 MB var in, analyses, and copies var back (BASELINE.md §4's
+    PCIe-inclusive definition).  `pinned`: page-locked host arrays (torch pin_memory), else
+    ordinary pageable numpy arrays as a Fortran host would pass them.  Detail only; never
+    `value`."""
+    if pinned:
+        def host(a):
+            t = torch.empty(a.shape, dtype=torch.float32, pin_memory=True)
+            t.copy_(torch.from_numpy(a))
+            return t.numpy()
+    else:
+        def host(a):
+            return np.array(a, np.float32, copy=True)
+    x, y, alt, var = (host(a) for a in (w.x, w.y, w.alt, w.var))
+    core = abi.Core(w.k, device=local)
+    core.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    slab = abi.make_slab(x, y, alt, var)
+    for _ in range(warmup):
+        core.analyze_var(w.vp, slab)
+    t0 = time.perf_counter()
+    stats = [core.analyze_var(w.vp, slab) for _ in range(steps)]
+    el = time.perf_counter() - t0
+    core.finalize()
+    return {"value": sum(s.points for s in stats) / el, "unit": "grid-points/s",
+            "ms_per_step": el / steps * 1e3, "steps": steps,
+            "ms_copy_per_step": sum(s.ms_copy for s in stats) / steps,
+            "host_arrays": "pinned (page-locked)" if pinned else "pageable numpy",
+            "bytes_per_step": int(x.nbytes + y.nbytes + alt.nbytes + 2 * var.nbytes)}
+
+
+def self_launch(n):
+    """Run this script as n ranks under torch.distributed.run (one process per GPU, rendezvous
+    on 127.0.0.1) and return their exit status.  The caller has not initialised HIP: the
+    ranks are fresh child processes, nothing is exec'd in place."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -256,17 +369,34 @@ def main():
                     help="also time one member<->column transpose of the variable (detail only)")
     ap.add_argument("--no-cycle", action="store_true",
                     help="skip the wall-clock-per-cycle detail (16 var_update entries)")
+    ap.add_argument("--no-detail-configs", action="store_true",
+                    help="skip the C4 / C5 / host-memory detail legs")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without a launcher: start the N ranks ourselves, before
+        # this process touches the GPU (it never initialises HIP; it only waits)
+        sys.exit(self_launch(args.gpus))
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    # (modulo the visible GPUs: one GPU can host a multi-rank rehearsal)
-    local = int(os.environ.get("LOCAL_RANK", 0)) % max(torch.cuda.device_count(), 1)
+    backend = os.environ.get("CWBL_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()  # (does not initialise HIP on this image)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to time "
+              f"{world} rank(s) as {args.gpus} GPU(s)", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if world > 1 and backend == "nccl" and ndev < world:
+        print(f"bench.py: {world} ranks need {world} distinct GPUs with RCCL, {ndev} visible "
+              f"(CWBL_DIST_BACKEND=gloo rehearses several ranks on one GPU)",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    # (gloo rehearsal only: ranks share the visible GPUs modulo their count)
+    local = int(os.environ.get("LOCAL_RANK", 0)) % max(ndev, 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         # RCCL over xGMI; CWBL_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU
-        backend = os.environ.get("CWBL_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -322,6 +452,22 @@ def main():
 
     tr_detail = time_transposes(core, w, k, rank, world, dev) if args.transposes else None
     cycle = None if args.no_cycle else time_cycle(core, w, world, dev, x, y, alt)
+    legs = {}
+    if not args.no_detail_configs and args.config == "c2":
+        # the other configurations on the same clock (detail; the library is re-initialised
+        # per leg, so the headline core is finished first)
+        del slab, var
+        core.finalize()
+        torch.cuda.empty_cache()
+        legs["c4"] = time_config("c4", rank, world, local, dev, steps=2, warmup=1)
+        torch.cuda.empty_cache()
+        legs["c5"] = time_config("c5", rank, world, local, dev, steps=2, warmup=1)
+        torch.cuda.empty_cache()
+        if world == 1:
+            legs["host_memory"] = {
+                "pageable": time_host_memory(w, local, steps=3, warmup=1, pinned=False),
+                "pinned": time_host_memory(w, local, steps=3, warmup=1, pinned=True)}
+        core = abi.Core(k, device=local)  # (finalised below)
 
     if rank == 0:
         jacobi = os.environ.get("CWBL_SOLVER") == "jacobi"
@@ -336,12 +482,13 @@ def main():
             kp = 40  # k = 25..32 run the KP = 40 record path (cwbl_init)
         tq4 = os.environ.get("CWBL_TQ4", "1")
         split = not jacobi and kp == 40 and tq4 != "0"
-        split128 = kp == 128 and k > 66 and os.environ.get("CWBL_BIG_SPLIT", "1") != "0"
-        kpair = (("assemble_record_kernel<40, 4>", "solve_tq40_kernel<40, 0>") if tq4 != "8" else
-                 ("solve_tq_kernel<40, false, 8>", "solve_tq4_kernel<40, 8>"))
+        # the host's rule (cwbl_analyze_var): KP = 96 / 128 split after kp - 64 steps when
+        # k > kp - 62, unless CWBL_BIG_SPLIT=0
+        split_big = kp in (96, 128) and k > kp - 62 and os.environ.get("CWBL_BIG_SPLIT", "1") != "0"
+        kpair = ("assemble_record_kernel<40, 4>", "solve_tq40_kernel<40, 0>")
         kname = (" + ".join(kpair) if split else
-                 "solve_tq_big_kernel<128, false, 64> + solve_tqb_tail_kernel<128, 64, 2>"
-                 if split128 else
+                 f"solve_tq_big_kernel<{kp}, false, {kp - 64}> + "
+                 f"solve_tqb_tail_kernel<{kp}, {kp - 64}, 2>" if split_big else
                  ("solve_kernel" if jacobi else
                   "solve_tq_kernel" if kp <= 64 else "solve_tq_big_kernel") + f"<{kp}, false>")
         traffic = None  # HBM bytes per launch from the committed PMC pass of this kernel
@@ -425,6 +572,7 @@ def main():
                 "obs_bcast_ms": bcast_ms,
                 "transposes": tr_detail,
                 "cycle": cycle,
+                **legs,
             },
             "cpu_baseline": None,
         }
@@ -436,6 +584,10 @@ def main():
             out["cpu_baseline"] = ref or port
             if ref:
                 out["detail"]["cpu_baseline_port"] = port
+            host = f"; host: {cpu_model()}, nproc {os.cpu_count()}, used {out['cpu_baseline']['cores']}"
+            for b in (ref, port):
+                if b:
+                    b["sample"] += host
         print(json.dumps(out), flush=True)
     core.finalize()
     if world > 1:

@@ -117,18 +117,20 @@ struct State {
   long long max_batch = 160000;
   bool max_batch_set = false;                         // CWBL_MAX_BATCH given: no ~6-batch rule
   DevBuf sx, sy, salt, svar;                          // slab staging (host-memory calls)
-  DevBuf bcol, byo, byb, bxb, bxa, bev;               // solve_batch staging
+  DevBuf bcol, byo, byb, bxb, bxa, bev, btri;         // solve_batch staging (btri: T per point)
   DevBuf qxyz, qnf, qidx, qr2;                        // search staging
   DevBuf quad;                                        // x^-1/2 quadrature tables
   DevBuf wsa;                                         // hand-off records (split KP=40 path)
   DevBuf flags;                                       // binned search: flagged points (+ count)
   bool binned = true;                                 // CWBL_SEARCH=tree: k-d tree search only
   bool jacobi = false;                                // CWBL_SOLVER=jacobi: eigen path
-  int tq4 = 1;  // CWBL_TQ4: KP=40 solve 0 = one kernel, 1 = assembly + tq40, 8 = hand-off after 8 steps
-  long long tq4_sub = 0;                              // CWBL_TQ4_SUB: hand-off batch (points)
+  int tq4 = 1;  // CWBL_TQ4: KP=40 solve 0 = one kernel, else assembly record + solve_tq40
+  long long tq4_sub = 0;                              // CWBL_TQ4_SUB: record batch (points)
   bool big_split = true;                              // CWBL_BIG_SPLIT=0: one-kernel KP=128 solve
   long long big_sub = 32768;                          // CWBL_BIG_SUB: KP=128 hand-off batch
   std::vector<hipEvent_t> events;
+  hipStream_t caller_stream = nullptr;                // cwbl_set_stream (null: legacy stream)
+  hipEvent_t order_ev = nullptr;                      // order_after_caller
 };
 
 State S;
@@ -204,12 +206,22 @@ int require_device() {
 }
 
 // The library's streams are non-blocking: they are not ordered after work the caller has
-// queued on the null stream, on its own streams (torch's current stream) or on a
-// collective's stream (an RCCL broadcast of the obs set).  Every entry point that reads or
-// writes caller device memory therefore first waits for all of the caller's queued work, so
-// device buffers may be passed as soon as their producers have been *queued*.  (Host-memory
-// calls need no wait: the caller's host arrays are complete when the call is made.)
-hipError_t order_after_caller() { return hipDeviceSynchronize(); }
+// queued on its own stream.  Every entry point that reads or writes caller device memory
+// therefore first makes the library's stream wait for an event recorded on the caller's
+// stream (cwbl_set_stream; the legacy null stream by default), so device buffers may be
+// passed as soon as their producers have been *queued* there.  Only that stream is waited
+// for: unrelated streams of the process (another rank's collectives, other compute) are not
+// (host-memory calls need no wait: the caller's host arrays are complete when the call is
+// made).
+hipError_t order_after_caller() {
+  if (!S.order_ev) {
+    hipError_t e = hipEventCreateWithFlags(&S.order_ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e = hipEventRecord(S.order_ev, S.caller_stream);
+  if (e != hipSuccess) return e;
+  return hipStreamWaitEvent(S.stream, S.order_ev, 0);
+}
 
 // Builds the trees of one family (build_tree, module_localization.f90:35-167) and their
 // column tables.  Appends TreeDesc entries.
@@ -345,11 +357,14 @@ void release_all() {
   if (S.tstream) (void)hipStreamDestroy(S.tstream);
   S.tstream = nullptr;
   for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.nbr_cnt2, &S.nbr_idx2, &S.info, &S.stats, &S.sx,
-                    &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev,
+                    &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev, &S.btri,
                     &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad, &S.wsa, &S.flags})
     b->release();
   for (hipEvent_t e : S.events) (void)hipEventDestroy(e);
   S.events.clear();
+  if (S.order_ev) (void)hipEventDestroy(S.order_ev);
+  S.order_ev = nullptr;
+  S.caller_stream = nullptr;
   if (S.stream) (void)hipStreamDestroy(S.stream);
   S.stream = nullptr;
   if (S.sstream) (void)hipStreamDestroy(S.sstream);
@@ -372,7 +387,7 @@ SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps,
   c.max_sweeps = 30;
   if (const char *e = std::getenv("CWBL_DEBUG_MAX_SWEEPS")) c.max_sweeps = std::atoi(e);
   c.quad_r = S.quad.as<double2>();
-  c.quad = c.quad_r ? c.quad_r + (size_t)2 * kQuadLevels * 32 : nullptr;  // 31 nodes
+  c.quad = c.quad_r;
   if (const char *e = std::getenv("CWBL_DEBUG_TQ_STOP")) c.debug_stop = std::atoi(e);
   if (const char *e = std::getenv("CWBL_DEBUG_STAGGER")) c.stagger = std::atoi(e);
   if (const char *e = std::getenv("CWBL_DEBUG_TQ_STEPS")) c.debug_steps = std::atoi(e);
@@ -423,10 +438,12 @@ int cwbl_init(const cwbl_init_params *p) {
   HIPCHK(hipStreamCreateWithFlags(&S.sstream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.tstream, hipStreamNonBlocking));
   {
-    std::vector<double2> tab((size_t)3 * kQuadLevels * 32);  // 15, 23, 31 nodes
-    for (int r = 0; r < 3; ++r)
+    std::vector<double2> tab((size_t)4 * kQuadLevels * kQuadStride);  // 15, 23, 31, 63 nodes
+    const int rounds[4] = {2, 3, 4, 8};
+    for (int r = 0; r < 4; ++r)
       for (int l = 1; l <= kQuadLevels; ++l)
-        quad_table(l, &tab[((size_t)r * kQuadLevels + (l - 1)) * 32], 8 * (r + 2) - 1);
+        quad_table(l, &tab[((size_t)r * kQuadLevels + (l - 1)) * kQuadStride],
+                   8 * rounds[r] - 1);
     HIPCHK(S.quad.ensure(tab.size() * sizeof(double2)));
     HIPCHK(hipMemcpy(S.quad.p, tab.data(), tab.size() * sizeof(double2), hipMemcpyHostToDevice));
   }
@@ -460,6 +477,12 @@ int cwbl_init(const cwbl_init_params *p) {
     S.max_batch_set = true;  // an explicit cap is used as given
   }
   S.inited = true;
+  return CWBL_OK;
+}
+
+int cwbl_set_stream(void *stream) {
+  if (int rc = require_device()) return rc;
+  S.caller_stream = static_cast<hipStream_t>(stream);
   return CWBL_OK;
 }
 
@@ -497,7 +520,7 @@ int cwbl_set_obs(const cwbl_obs_set *o) {
     t.xyz.resize(3 * n);
     if (n) {
       if (mem == CWBL_MEM_DEVICE)
-        HIPCHK(hipMemcpy(t.xyz.data(), g.xyz, 3 * n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(t.xyz.data(), g.xyz, 3 * n * 4, hipMemcpyDeviceToHost, S.stream));
       else
         std::memcpy(t.xyz.data(), g.xyz, 3 * n * 4);
     }
@@ -521,7 +544,7 @@ int cwbl_set_obs(const cwbl_obs_set *o) {
     t.xyz.resize(3 * n);
     if (n) {
       if (mem == CWBL_MEM_DEVICE)
-        HIPCHK(hipMemcpy(t.xyz.data(), r.xyz, 3 * n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(t.xyz.data(), r.xyz, 3 * n * 4, hipMemcpyDeviceToHost, S.stream));
       else
         std::memcpy(t.xyz.data(), r.xyz, 3 * n * 4);
     }
@@ -672,7 +695,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   // busy, the four-point solve is latency-bound).  Two record and two info buffers; an
   // assembly waits for the solve two record batches back (record reuse) and for the info
   // reduction two search batches back (info reuse).
-  const bool conc = S.tq40_streams && S.tq4 && S.tq4 != 8 && S.kp == kTq4KP && !S.jacobi;
+  const bool conc = S.tq40_streams && S.tq4 && S.kp == kTq4KP && !S.jacobi;
   int nrec = 0;                 // record batches so far
   std::vector<int> rec_done;    // cevent after each record batch's solve (on S.tstream)
   std::vector<int> info_done;   // cevent after each search batch's info reduction
@@ -739,10 +762,8 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       long long Bs = (nb + nsub - 1) / nsub;
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
       Bs = std::min<long long>(Bs, 1 << 19);
-      const bool rec = S.tq4 != 8;  // AsmRecord + solve_tq40_kernel, else Tq4Handoff
       // (+1: the spare record of solve_tq40_kernel's lanes past the batch)
-      const size_t wbytes = (size_t)(Bs + 1) * 8 *
-                            (rec ? AsmRecord<kTq4KP>::WORDS : Tq4Handoff<kTq4KP, kTq4J0>::WORDS);
+      const size_t wbytes = (size_t)(Bs + 1) * 8 * AsmRecord<kTq4KP>::WORDS;
       HIPCHK(S.wsa.ensure(wbytes));
       if (conc) HIPCHK(S.wsa2.ensure(wbytes));
       int2 *binfo = conc && (bi & 1) ? S.info2.as<int2>() : S.info.as<int2>();
@@ -767,18 +788,12 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
           rec_done.push_back(cev + 1);
           cev += 2;
           ++nrec;
-        } else if (rec) {
+        } else {
           HIPCHK(launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
                                         ncnt + s0 * nt, nidx + s0 * list_cap,
                                         S.info.as<int2>() + s0, S.wsa.as<double>()));
           HIPCHK(launch_solve_tq40(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
                                    S.info.as<int2>() + s0));
-        } else {
-          HIPCHK(launch_assemble_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
-                                         ncnt + s0 * nt, nidx + s0 * list_cap,
-                                         S.info.as<int2>() + s0, S.wsa.as<double>()));
-          HIPCHK(launch_solve_tq4(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
-                                  S.info.as<int2>() + s0));
         }
       }
     } else
@@ -855,16 +870,14 @@ int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const 
   if (npts < 0 || (npts > 0 && (!col_off || !xb || !xa)))
     return fail(CWBL_ERR_ARG, "cwbl_solve_batch: bad arguments");
   if (npts == 0) return CWBL_OK;
-  if (evals && S.kp > kMaxWaveKP)
-    return fail(CWBL_ERR_UNSUPPORTED,
-                "cwbl_solve_batch: eigenvalue output needs k <= %d (the Jacobi path)", kMaxWaveKP);
   const size_t k = (size_t)S.k;
   std::vector<long long> hoff;
   const long long *doff = col_off;
   long long ncol;
   if (memory == CWBL_MEM_DEVICE) {
     HIPCHK(order_after_caller());
-    HIPCHK(hipMemcpy(&ncol, col_off + npts, 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(&ncol, col_off + npts, 8, hipMemcpyDeviceToHost, S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
   } else {
     ncol = col_off[npts];
     for (int i = 0; i < npts; ++i)
@@ -886,15 +899,25 @@ int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const 
   }
   HIPCHK(S.info.ensure((size_t)npts * sizeof(int2)));
   SolveConsts c = solve_consts(inflat, use_rtpp, rtpp_alpha, use_rtps, rtps_alpha);
+  // Eigenvalues (dsyevd's ascending eval, module_eigen.f90:48-56): from the tridiagonal T the
+  // tq kernels form, by bisection (launch_tridiag_eigvals), at every k; CWBL_SOLVER=jacobi
+  // (k <= 64) takes them from the Jacobi eigensolver instead.
+  const bool jacobi = S.jacobi && S.kp <= kMaxWaveKP;
+  double *tri = nullptr;
+  if (dev && !jacobi) {
+    HIPCHK(S.btri.ensure((size_t)npts * 2 * S.kp * sizeof(double)));
+    tri = S.btri.as<double>();
+  }
   if (S.kp > kMaxWaveKP)
     HIPCHK(launch_solve_tq_big(S.stream, S.kp, true, nullptr, c, SlabDev{}, 0, npts, nullptr,
-                               nullptr, doff, dyo, dyb, dxb, dxa, S.info.as<int2>()));
-  else if (dev || S.jacobi)  // eigenvalues requested: the Jacobi eigensolver path
+                               nullptr, doff, dyo, dyb, dxb, dxa, S.info.as<int2>(), tri));
+  else if (jacobi)
     HIPCHK(launch_solve_assembled(S.stream, S.kp, c, npts, doff, dyo, dyb, dxb, dxa, dev,
                                   S.info.as<int2>()));
   else
     HIPCHK(launch_solve_tq(S.stream, S.kp, true, nullptr, c, SlabDev{}, 0, npts, nullptr,
-                           nullptr, doff, dyo, dyb, dxb, dxa, S.info.as<int2>()));
+                           nullptr, doff, dyo, dyb, dxb, dxa, S.info.as<int2>(), tri));
+  if (tri) HIPCHK(launch_tridiag_eigvals(S.stream, S.kp, S.k, npts, tri, dev));
   if (memory != CWBL_MEM_DEVICE) {
     HIPCHK(hipMemcpyAsync(xa, dxa, (size_t)npts * k * 4, hipMemcpyDeviceToHost, S.stream));
     if (evals)

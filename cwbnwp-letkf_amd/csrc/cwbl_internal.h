@@ -86,9 +86,9 @@ struct SolveConsts {
   float nmember_inv;          // 1.0/k (module_param.f90:245)
   float r2;                   // gc1999**2
   int   max_sweeps;           // Jacobi sweep cap (CWBL_DEBUG_MAX_SWEEPS overrides; ablation only)
-  const double2 *quad;        // [kQuadLevels][32] (t2, w) of the x^-1/2 rule (solve_tq_kernel)
-  const double2 *quad_r;      // [3][kQuadLevels][32]: the rules of 15, 23, 31 nodes (= quad),
-                              // 8 R - 1 nodes for R = 2, 3, 4 rounds of solve_tq40_kernel
+  const double2 *quad;        // = quad_r (non-null once the tables are built)
+  const double2 *quad_r;      // [4][kQuadLevels][kQuadStride] (t2, w) of the x^-1/2 rules of
+                              // 8 R - 1 nodes, R = 2, 3, 4, 8 (quad_rule)
   int   stagger;              // CWBL_DEBUG_STAGGER: start-phase offset unit in cycles (experiment)
   int   debug_stop;           // CWBL_DEBUG_TQ_STOP: 1 = after assembly, 2 = after
                               // tridiagonalisation, 3 = after quadrature, 4 = after the first
@@ -97,15 +97,28 @@ struct SolveConsts {
                               // in solve_tq_big_kernel (timing ablation only)
 };
 
-// Inverse-square-root quadrature of solve_tq_kernel (quad_tables.cpp): level L = 1..12
-// covers spectra with max/min <= 10^L using kQuadNodes nodes (slot 31 of a level is unused).
+// Inverse-square-root quadrature of the tq kernels (quad_tables.cpp): level L = 1..kQuadLevels
+// covers spectrum bounds with max/min <= 10^L.  The one-wavefront kernels run kQuadNodes nodes
+// per pass (64 lanes = 32 nodes x 2 sides, node 31 of the first pass the exact T^-1 solve):
+// one pass (31 nodes) up to level kQuadLevels31, two (63 nodes) above; beyond 10^24 a point is
+// counted non-converged.  Tables hold kQuadStride (t2, w) entries per level.
 constexpr int kQuadNodes = 31;
-constexpr int kQuadLevels = 12;
-void quad_table(int level, double2 *out32, int nodes = kQuadNodes);
+constexpr int kQuadLevels = 24;
+constexpr int kQuadLevels31 = 12;
+constexpr int kQuadStride = 64;
+void quad_table(int level, double2 *out64, int nodes = kQuadNodes);
 // Rounds of 8 nodes (the last round's slot 7 is the exact T^-1 solve) solve_tq40_kernel runs
-// at a level: the (8 R - 1)-node rule is as accurate as the 31-node one there (relative error
-// <= 1e-15; tests/test_quadrature.py)
-__host__ __device__ constexpr int quad_rounds(int level) { return level <= 2 ? 2 : level == 3 ? 3 : 4; }
+// at a level: the (8 R - 1)-node rule is as accurate as the 31-node one up to level 12
+// (relative error <= 1e-15 at levels 1..3; tests/test_quadrature.py), 63 nodes above.
+__host__ __device__ constexpr int quad_rounds(int level) {
+  return level <= 2 ? 2 : level == 3 ? 3 : level <= kQuadLevels31 ? 4 : 8;
+}
+// passes of the one-wavefront kernels' rule (31 nodes per pass + the exact solve)
+__host__ __device__ constexpr int quad_passes(int level) { return level <= kQuadLevels31 ? 1 : 2; }
+// the (8 R - 1)-node rule of a level, R = 2, 3, 4 or 8
+__host__ __device__ inline const double2 *quad_rule(const double2 *quad_r, int R, int level) {
+  return quad_r + ((size_t)(R == 8 ? 3 : R - 2) * kQuadLevels + (level - 1)) * kQuadStride;
+}
 
 // Point enumeration of a slab: g = i + ix_lim*(j + iy_lim*kz).
 struct SlabDev {
@@ -165,45 +178,21 @@ hipError_t launch_solve_assembled(hipStream_t s, int kp, SolveConsts c, int npts
                                   const float *xb, float *xa, double *evals, int2 *info);
 
 // Tridiagonalisation + quadrature solve (cwbl_tq.hip); same data contract as the two
-// launchers above, no eigenvalue output.
+// launchers above.  `tri` (assembled mode only): T of every point for launch_tridiag_eigvals.
 hipError_t launch_solve_tq(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,
                            SolveConsts c, SlabDev slab, long long g0, int npts,
                            const int *nbr_cnt, const int *nbr_idx,
                            const long long *col_off, const float *yo, const float *yb,
-                           const float *xb, float *xa, int2 *info);
+                           const float *xb, float *xa, int2 *info, double *tri = nullptr);
 
-// Split form of the KP = 40 slab path: solve_tq_kernel<40, false, kTq4J0> assembles A and
-// runs the first kTq4J0 Householder steps (4x4 register blocks, one point per wavefront),
-// then hands the rest over through the workspace (Tq4Handoff, info[gi] = (p, 0));
-// solve_tq4_kernel (cwbl_tq4.hip) finishes the tridiagonalisation on the 32 x 32 trailing
-// matrix with four points per wavefront, solves and writes var in place.
-constexpr int kTq4KP = 40;
-constexpr int kTq4J0 = 8;
-// fp64 words of one point's hand-off record
-template <int KP, int J0>
-struct Tq4Handoff {
-  static constexpr int KT = KP - J0;            // trailing rows
-  static constexpr int NT = KT * (KT + 1) / 2;  // trailing A, packed lower (rows J0..KP-1)
-  static constexpr int HV = NT;                 // reflectors 0..J0-1 as KP-rows (0 above j+1)
-  static constexpr int D = HV + J0 * KP;        // d_0 .. d_{J0-1}
-  static constexpr int E = D + J0;              // c(j, j+1), j = 0..J0-1
-  static constexpr int TAU = E + J0;            // tau_0 .. tau_{J0-1}
-  static constexpr int U1 = TAU + J0;           // Q_J0^T b1 (KP)
-  static constexpr int U2 = U1 + KP;            // Q_J0^T x' (KP)
-  static constexpr int WORDS = (U2 + KP + 1) / 2 * 2;
-};
-hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
-                                   SlabDev slab, long long g0, int npts, const int *nbr_cnt,
-                                   const int *nbr_idx, int2 *info, double *ws);
-hipError_t launch_solve_tq4(hipStream_t s, int kp, SolveConsts c, SlabDev slab, long long g0,
-                            int npts, const double *ws, int2 *info);
+constexpr int kTq4KP = 40;  // KP of the split record path (k = 25..40)
 
 // The default KP = 40 split: assemble_record_kernel (cwbl_tq.hip) only stages and assembles,
 // one point per wavefront, and writes A = inflat I + Yb Yb^T (packed lower, the padding's
 // diagonal 1) and b1 = Yb d; solve_tq40_kernel (cwbl_tq40.hip) runs the whole
 // tridiagonalisation with four points per wavefront (the first kTq40J0 steps on full rows
-// J0..KP-1 plus the prefix rows' top-left block, then the same layout as solve_tq4_kernel),
-// solves and writes var in place.
+// J0..KP-1 plus the prefix rows' top-left block, then 16-lane rows of the trailing 32 x 32
+// matrix), solves and writes var in place.
 constexpr int kTq40J0 = 8;
 template <int KP>
 struct AsmRecord {
@@ -252,7 +241,13 @@ hipError_t launch_solve_tq_big(hipStream_t s, int kp, bool assembled, const Tree
                                SolveConsts c, SlabDev slab, long long g0, int npts,
                                const int *nbr_cnt, const int *nbr_idx,
                                const long long *col_off, const float *yo, const float *yb,
-                               const float *xb, float *xa, int2 *info);
+                               const float *xb, float *xa, int2 *info, double *tri = nullptr);
+
+// Eigenvalues of the tridiagonal T = Q^T A Q the tq kernels form (assembled mode, `tri`:
+// per point d_0..d_{KP-1} then c(i, i+1), 2 KP words): ascending, by Sturm-count bisection
+// in fp64 (cwbl_eig.hip), i.e. the eigenvalues of A that dsyevd returns (module_eigen.f90:49)
+hipError_t launch_tridiag_eigvals(hipStream_t s, int kp, int k, int npts, const double *tri,
+                                  double *evals);
 
 // The analysis search from uniform bins: the same fixed-radius sets as launch_search (the
 // same fp32 distances and <= r2 test) in bin order, which differs from kdtree2's visiting

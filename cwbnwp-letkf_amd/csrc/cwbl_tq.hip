@@ -98,10 +98,9 @@ struct TqOccupancy {
   static constexpr int kWaves = KP <= 40 ? 4 : KP <= 48 ? 3 : 2;
 };
 
-// HS > 0: after the assembly and the first HS Householder steps, hand the trailing matrix,
-// the reflectors, T so far and Q^T b1, Q^T x' over to solve_tq4_kernel (cwbl_tq4.hip)
-// through ws (Tq4Handoff); info[gi] = (p, 0).
-template <int KP, bool ASSEMBLED, int HS = 0>
+// ws (assembled mode, nullable): T of every point (d, then c(i, i+1); 2 KP words) for the
+// eigenvalue output of cwbl_solve_batch (launch_tridiag_eigvals).
+template <int KP, bool ASSEMBLED>
 __global__ void __launch_bounds__(64, TqOccupancy<KP>::kWaves)
 solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab, long long g0,
                 int npts, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
@@ -168,6 +167,10 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
       if (lane == 0 && info) info[gi] = make_int2(0, 0);
       if constexpr (ASSEMBLED) {
         if (lane < k) xa_out[(long long)gi * k + lane] = xbl;
+        if (ws && lane < KP) {  // T = A = inflat I (no observation)
+          ws[(long long)gi * 2 * KP + lane] = lane < k ? (double)c.inflat : 1.0;
+          ws[(long long)gi * 2 * KP + KP + lane] = 0.0;
+        }
       }
       return;
     }
@@ -465,48 +468,12 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   };
   // unrolled by the block width, so that the pivot column's registers are known statically
   using std::false_type, std::true_type, std::integral_constant;
-  const int jend1 = HS > 0 ? (k < HS ? k : HS) : (k < J0T ? k : J0T);
+  const int jend1 = k < J0T ? k : J0T;
   for (int j = 0; j < jend1; j += 4) {
     step(j, false_type{}, integral_constant<int, 0>{}, acc);
     if (j + 1 < jend1) step(j + 1, false_type{}, integral_constant<int, 1>{}, acc);
     if (j + 2 < jend1) step(j + 2, false_type{}, integral_constant<int, 2>{}, acc);
     if (j + 3 < jend1) step(j + 3, false_type{}, integral_constant<int, 3>{}, acc);
-  }
-  if constexpr (HS > 0) {  // hand-off (Tq4Handoff) after HS steps
-    static_assert(HS % 4 == 0 && HS <= J0T, "hand-off at a block boundary");
-    using HO = Tq4Handoff<KP, HS>;
-    double *__restrict__ w = ws + (long long)gi * HO::WORDS;
-    constexpr int JB = HS / 4;
-#pragma unroll
-    for (int it = 0; it < NBL; ++it) {  // trailing blocks, packed lower
-      if (lane + 64 * it < NBLK && bj[it] >= JB) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int a = 4 * (bi[it] - JB) + r, b = 4 * (bj[it] - JB) + q;
-            if (a >= b) w[a * (a + 1) / 2 + b] = acc[it][4 * r + q];
-          }
-      }
-    }
-    __syncthreads();
-    if (lane < KP) {
-      for (int j = 0; j < HS; ++j) {  // reflector j (never stored when tau = 0: H = I)
-        const double t = sm.tau[j];
-        const int off = j * (k - 1) - j * (j - 1) / 2 + lane - (j + 1);
-        w[HO::HV + j * KP + lane] =
-            (t != 0.0 && lane > j && lane < k) ? sm.u.reg[SM::hv_off(0) + off] : 0.0;
-      }
-      w[HO::U1 + lane] = ub;
-      w[HO::U2 + lane] = ux;
-    }
-    if (lane < HS) {
-      w[HO::D + lane] = sm.tq[lane][0];
-      w[HO::E + lane] = sm.tq[lane + 1][1];
-      w[HO::TAU + lane] = sm.tau[lane];
-    }
-    if (lane == 0) info[gi] = make_int2(ptot, 0);
-    return;
   }
   if constexpr (J0T < KP) {
     static_assert(J0T % 2 == 0, "2x2 phase alignment");
@@ -523,6 +490,12 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     sm.tq[lane][3] = ux;
   }
   __syncthreads();
+  if constexpr (ASSEMBLED) {  // T for the eigenvalue output (cwbl_solve_batch)
+    if (ws && lane < KP) {
+      ws[(long long)gi * 2 * KP + lane] = sm.tq[lane][0];           // d_i
+      ws[(long long)gi * 2 * KP + KP + lane] = sm.tq[lane + 1][1];  // c(i, i+1)
+    }
+  }
 
   if (c.debug_stop == 2) {
     if (lane == 0 && info) info[gi] = make_int2(ptot, (int)(trace + ux + ub));
@@ -540,52 +513,59 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     ++level;
   }
   const int node = lane & 31, side = lane >> 5;
-  double sigma = 0.0, omega = 0.0;
-  if (node < kQuadNodes) {
-    const double2 tw = c.quad[(level - 1) * 32 + node];
-    sigma = m * tw.x;
-    omega = sqrt(m) * tw.y;
-  }
+  // one pass of 31 nodes (+ the exact solve on node 31) up to level kQuadLevels31, a second
+  // pass with nodes 31..62 of the 63-node rule above (quad_passes; wave-uniform)
+  const int npass = quad_passes(level);
+  const double2 *rule = quad_rule(c.quad_r, npass == 1 ? 4 : 8, level);
   // lane side 0 walks rows 0, 1, .. H-1; side 1 walks rows KP-1, KP-2, .. H (mirrored).
   // Forward elimination towards the middle keeps, per row, h_t = g_t / dl_t and
   // m_t = c_{t+1} / dl_t, so that back substitution is x_t = h_t - m_t x_{t+1}.
   const int dir = side ? -4 : 4;
   const double *q = &sm.tq[side ? KP - 1 : 0][0];
   const int cs = side ? 5 : 1;  // coupling with the previous mirrored row: c(i-1,i) / c(i,i+1)
-  double hh[H], mm[H];
-  double dl = q[0] + sigma;
-  double gt = q[3];
-  double rdl = rcp64(dl);
-#pragma unroll
-  for (int t = 1; t < H; ++t) {
-    const double *qt = q + dir * t;
-    const double ct = qt[cs];
-    const double l = ct * rdl;
-    hh[t - 1] = gt * rdl;
-    mm[t - 1] = l;  // = c_t / dl_{t-1}
-    asm volatile("" : "+v"(hh[t - 1]));  // materialise now: g_{t-1} and 1/dl_{t-1} die here
-    dl = fma(-l, ct, qt[0] + sigma);
-    gt = fma(-l, gt, qt[3]);
-    rdl = rcp64(dl);
-    __builtin_amdgcn_sched_barrier(0);  // keep the recurrence in order: bounded live ranges
-  }
-  // meeting rows H-1 (top) and H (bottom): 2x2 solve with the partner lane's pivot
-  const double cm = sm.tq[H][1];
-  const double dlo = __shfl_xor(dl, 32, 64), go = __shfl_xor(gt, 32, 64);
-  double xv = (gt * dlo - cm * go) / fma(dl, dlo, -cm * cm);
   double *ym = Ym + side * H, *zm = Zm + side * H;
-  {
-    const double ys = half_sum_dpp(omega * xv);
-    if (node == 0) ym[H - 1] = ys;
-    if (node == 31) zm[H - 1] = xv;
-  }
+  for (int pass = 0; pass < npass; ++pass) {
+    const bool exact = pass == 0 && node == 31;
+    double sigma = 0.0, omega = 0.0;
+    if (!exact) {
+      const double2 tw = rule[31 * pass + node];
+      sigma = m * tw.x;
+      omega = sqrt(m) * tw.y;
+    }
+    double hh[H], mm[H];
+    double dl = q[0] + sigma;
+    double gt = q[3];
+    double rdl = rcp64(dl);
 #pragma unroll
-  for (int t = H - 2; t >= 0; --t) {
-    xv = fma(-mm[t], xv, hh[t]);
-    const double ys = half_sum_dpp(omega * xv);
-    if (node == 0) ym[t] = ys;
-    if (node == 31) zm[t] = xv;
-    __builtin_amdgcn_sched_barrier(0);
+    for (int t = 1; t < H; ++t) {
+      const double *qt = q + dir * t;
+      const double ct = qt[cs];
+      const double l = ct * rdl;
+      hh[t - 1] = gt * rdl;
+      mm[t - 1] = l;  // = c_t / dl_{t-1}
+      asm volatile("" : "+v"(hh[t - 1]));  // materialise now: g_{t-1} and 1/dl_{t-1} die here
+      dl = fma(-l, ct, qt[0] + sigma);
+      gt = fma(-l, gt, qt[3]);
+      rdl = rcp64(dl);
+      __builtin_amdgcn_sched_barrier(0);  // keep the recurrence in order: bounded live ranges
+    }
+    // meeting rows H-1 (top) and H (bottom): 2x2 solve with the partner lane's pivot
+    const double cm = sm.tq[H][1];
+    const double dlo = __shfl_xor(dl, 32, 64), go = __shfl_xor(gt, 32, 64);
+    double xv = (gt * dlo - cm * go) / fma(dl, dlo, -cm * cm);
+    {
+      const double ys = half_sum_dpp(omega * xv);
+      if (node == 0) ym[H - 1] = pass ? ym[H - 1] + ys : ys;
+      if (exact) zm[H - 1] = xv;
+    }
+#pragma unroll
+    for (int t = H - 2; t >= 0; --t) {
+      xv = fma(-mm[t], xv, hh[t]);
+      const double ys = half_sum_dpp(omega * xv);
+      if (node == 0) ym[t] = pass ? ym[t] + ys : ys;
+      if (exact) zm[t] = xv;
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   __syncthreads();
   const int wi = lane < H ? lane : H + (KP - 1 - lane);  // walk slot of row `lane`
@@ -658,17 +638,6 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   }
   // info.y: decade of the quadrature rule (negative when M/m exceeds the last table)
   if (lane == 0 && info) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
-}
-
-hipError_t launch_assemble_handoff(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
-                                   SlabDev slab, long long g0, int npts, const int *nbr_cnt,
-                                   const int *nbr_idx, int2 *info, double *ws) {
-  if (npts <= 0) return hipSuccess;
-  if (kp != kTq4KP) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((solve_tq_kernel<kTq4KP, false, kTq4J0>), dim3(npts), dim3(64), 0, s,
-                     trees, c, slab, g0, npts, nbr_cnt, nbr_idx, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, info, ws);
-  return hipGetLastError();
 }
 
 // Stage + assemble only (the default KP = 40 split): the MFMA tiles of [Yb; yo][Yb; yo]^T go
@@ -769,10 +738,10 @@ static hipError_t launch_tq_kp(hipStream_t s, bool assembled, const TreeDesc *tr
                                SolveConsts c, SlabDev slab, long long g0, int npts,
                                const int *nbr_cnt, const int *nbr_idx,
                                const long long *col_off, const float *yo, const float *yb,
-                               const float *xb, float *xa, int2 *info) {
+                               const float *xb, float *xa, int2 *info, double *tri) {
   if (assembled)
     hipLaunchKernelGGL((solve_tq_kernel<KP, true>), dim3(npts), dim3(64), 0, s, trees, c, slab,
-                       g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa, info);
+                       g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa, info, tri);
   else
     hipLaunchKernelGGL((solve_tq_kernel<KP, false>), dim3(npts), dim3(64), 0, s, trees, c,
                        slab, g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa, info);
@@ -783,13 +752,13 @@ hipError_t launch_solve_tq(hipStream_t s, int kp, bool assembled, const TreeDesc
                            SolveConsts c, SlabDev slab, long long g0, int npts,
                            const int *nbr_cnt, const int *nbr_idx,
                            const long long *col_off, const float *yo, const float *yb,
-                           const float *xb, float *xa, int2 *info) {
+                           const float *xb, float *xa, int2 *info, double *tri) {
   if (npts <= 0) return hipSuccess;
-  if (c.quad == nullptr) return hipErrorInvalidValue;
+  if (c.quad == nullptr || (tri && !assembled)) return hipErrorInvalidValue;
 #define CWBL_TQ_CASE(K)                                                                      \
   case K:                                                                                    \
     return launch_tq_kp<K>(s, assembled, trees, c, slab, g0, npts, nbr_cnt, nbr_idx,         \
-                           col_off, yo, yb, xb, xa, info);
+                           col_off, yo, yb, xb, xa, info, tri);
   switch (kp) {
     CWBL_TQ_CASE(8)
     CWBL_TQ_CASE(16)

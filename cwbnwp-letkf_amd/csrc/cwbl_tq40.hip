@@ -453,9 +453,9 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   // rounds of 8 nodes: the wave's largest need (quad_rounds) over its four points, with the
   // (8 R - 1)-node rule of each point's own level; slot 7 of the last round is T^-1 u2
   const int rp = quad_rounds(level);
-  const int R = __ballot(rp == 4) ? 4 : __ballot(rp == 3) ? 3 : 2;  // wave-uniform
-  const int NQ = 8 * R - 1;
-  const double2 *qtab = c.quad_r + ((size_t)(R - 2) * kQuadLevels + (level - 1)) * 32;
+  const int R = __ballot(rp == 8) ? 8 : __ballot(rp == 4) ? 4 : __ballot(rp == 3) ? 3 : 2;
+  const int NQ = 8 * R - 1;  // (R is wave-uniform)
+  const double2 *qtab = quad_rule(c.quad_r, R, level);
   const int side = l >> 3, n8 = l & 7;
   const double(*T)[4] = sm.tq[q];
   const double *tq0 = &T[side ? KP - 1 : 0][0];

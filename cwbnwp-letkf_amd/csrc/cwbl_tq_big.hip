@@ -295,6 +295,10 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     if (tid == 0 && info) info[gi] = make_int2(0, 0);
     if constexpr (ASSEMBLED) {
       if (tid < k) xa_out[(long long)gi * k + tid] = xbl;
+      if (ws && tid < KP) {  // T = A = inflat I (no observation)
+        ws[(long long)gi * 2 * KP + tid] = tid < k ? (double)c.inflat : 1.0;
+        ws[(long long)gi * 2 * KP + KP + tid] = 0.0;
+      }
     }
     return;
   }
@@ -548,6 +552,12 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     sm.tq[tid][3] = ux;
   }
   __syncthreads();
+  if constexpr (ASSEMBLED && HS == 0) {  // T for the eigenvalue output (cwbl_solve_batch)
+    if (ws && tid < KP) {
+      ws[(long long)gi * 2 * KP + tid] = sm.tq[tid][0];           // d_i
+      ws[(long long)gi * 2 * KP + KP + tid] = sm.tq[tid + 1][1];  // c(i, i+1)
+    }
+  }
 
   if (c.debug_stop == 2) {
     if (tid == 0 && info) info[gi] = make_int2(ptot, (int)(trace + ux + ub));
@@ -564,9 +574,15 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   }
   if (wave == 0) {
     const int node = lane & 31, side = lane >> 5;
+    // one pass of 31 nodes (+ the exact solve on node 31) up to level kQuadLevels31, a
+    // second pass with nodes 31..62 of the 63-node rule above (quad_passes; wave-uniform)
+    const int npass = quad_passes(level);
+    const double2 *rule = quad_rule(c.quad_r, npass == 1 ? 4 : 8, level);
+    for (int pass = 0; pass < npass; ++pass) {
+    const bool exact = pass == 0 && node == 31;
     double sigma = 0.0, omega = 0.0;
-    if (node < kQuadNodes) {
-      const double2 tw = c.quad[(level - 1) * 32 + node];
+    if (!exact) {
+      const double2 tw = rule[31 * pass + node];
       sigma = m * tw.x;
       omega = sqrt(m) * tw.y;
     }
@@ -613,10 +629,11 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
         const int t = S * s + i;
         if (t != H - 1) xv = fma(-mmv[i], xv, hh[i]);
         const double ys = half_sum_dpp(omega * xv);
-        if (node == 0) ym[t] = ys;
-        if (node == 31) zm[t] = xv;
+        if (node == 0) ym[t] = pass ? ym[t] + ys : ys;
+        if (exact) zm[t] = xv;
       }
     }
+    }  // pass
   }
   __syncthreads();
   const int wi = tid < H ? tid : H + (KP - 1 - tid);
@@ -744,11 +761,11 @@ static hipError_t launch_big_kp(hipStream_t s, bool assembled, const TreeDesc *t
                                 SolveConsts c, SlabDev slab, long long g0, int npts,
                                 const int *nbr_cnt, const int *nbr_idx,
                                 const long long *col_off, const float *yo, const float *yb,
-                                const float *xb, float *xa, int2 *info) {
+                                const float *xb, float *xa, int2 *info, double *tri) {
   if (assembled)
     hipLaunchKernelGGL((solve_tq_big_kernel<KP, true>), dim3(npts), dim3(kBigThreads), 0, s,
                        trees, c, slab, g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa,
-                       info);
+                       info, tri);
   else
     hipLaunchKernelGGL((solve_tq_big_kernel<KP, false>), dim3(npts), dim3(kBigThreads), 0, s,
                        trees, c, slab, g0, npts, nbr_cnt, nbr_idx, col_off, yo, yb, xb, xa,
@@ -776,16 +793,16 @@ hipError_t launch_solve_tq_big(hipStream_t s, int kp, bool assembled, const Tree
                                SolveConsts c, SlabDev slab, long long g0, int npts,
                                const int *nbr_cnt, const int *nbr_idx,
                                const long long *col_off, const float *yo, const float *yb,
-                               const float *xb, float *xa, int2 *info) {
+                               const float *xb, float *xa, int2 *info, double *tri) {
   if (npts <= 0) return hipSuccess;
-  if (c.quad == nullptr) return hipErrorInvalidValue;
+  if (c.quad == nullptr || (tri && !assembled)) return hipErrorInvalidValue;
   switch (kp) {
     case 96:
       return launch_big_kp<96>(s, assembled, trees, c, slab, g0, npts, nbr_cnt, nbr_idx,
-                               col_off, yo, yb, xb, xa, info);
+                               col_off, yo, yb, xb, xa, info, tri);
     case 128:
       return launch_big_kp<128>(s, assembled, trees, c, slab, g0, npts, nbr_cnt, nbr_idx,
-                                col_off, yo, yb, xb, xa, info);
+                                col_off, yo, yb, xb, xa, info, tri);
     default:
       return hipErrorInvalidValue;
   }

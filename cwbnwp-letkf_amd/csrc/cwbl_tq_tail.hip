@@ -252,9 +252,15 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   }
   {
     const int node = l & 31, side = l >> 5;
+    // one pass of 31 nodes (+ the exact solve on node 31) up to level kQuadLevels31, a
+    // second pass with nodes 31..62 of the 63-node rule above (quad_passes; wave-uniform)
+    const int npass = quad_passes(level);
+    const double2 *rule = quad_rule(c.quad_r, npass == 1 ? 4 : 8, level);
+    for (int pass = 0; pass < npass; ++pass) {
+    const bool exact = pass == 0 && node == 31;
     double sigma = 0.0, omega = 0.0;
-    if (node < kQuadNodes) {
-      const double2 tw = c.quad[(level - 1) * 32 + node];
+    if (!exact) {
+      const double2 tw = rule[31 * pass + node];
       sigma = m * tw.x;
       omega = sqrt(m) * tw.y;
     }
@@ -299,10 +305,11 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         const int t = S * s + i;
         if (t != H - 1) xv = fma(-mmv[i], xv, hh[i]);
         const double ys = half_sum_dpp(omega * xv);
-        if (node == 0) ym[t] = ys;
-        if (node == 31) zm[t] = xv;
+        if (node == 0) ym[t] = pass ? ym[t] + ys : ys;
+        if (exact) zm[t] = xv;
       }
     }
+    }  // pass
   }
   __syncthreads();
   // rows l (slot 0) and J0 + l (slot 1) in walk order: side 1 walks KP-1 .. H

@@ -84,7 +84,7 @@ class Stats(C.Structure):
 
 
 #: exported symbols of the product library (include/cwb_letkf_core.h)
-EXPORTS = ["cwbl_init", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch", "cwbl_search",
+EXPORTS = ["cwbl_init", "cwbl_set_stream", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch", "cwbl_search",
            "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
            "cwbl_member_sum", "cwbl_scale",
            "cwbl_finalize", "cwbl_last_error", "cwbl_abi_version"]
@@ -250,6 +250,7 @@ def load_library(path=None):
     vp, cp = C.c_void_p, C.c_char_p
     lib.cwbl_init.argtypes = [C.POINTER(InitParams)]
     lib.cwbl_set_obs.argtypes = [C.POINTER(ObsSet)]
+    lib.cwbl_set_stream.argtypes = [vp]
     lib.cwbl_analyze_var.argtypes = [C.POINTER(VarParams), C.POINTER(Slab), C.POINTER(Stats)]
     lib.cwbl_solve_batch.argtypes = [C.c_int, vp, vp, vp, vp, C.c_float, C.c_int, C.c_float,
                                      C.c_int, C.c_float, vp, vp, C.c_int]
@@ -263,7 +264,7 @@ def load_library(path=None):
     lib.cwbl_finalize.argtypes = []
     lib.cwbl_last_error.restype = cp
     lib.cwbl_abi_version.restype = C.c_int
-    for fn in ("cwbl_init", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch",
+    for fn in ("cwbl_init", "cwbl_set_stream", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch",
                "cwbl_search", "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
                "cwbl_member_sum", "cwbl_scale", "cwbl_finalize"):
         getattr(lib, fn).restype = C.c_int
@@ -291,6 +292,12 @@ class Core:
         if rc != 0:
             msg = self.lib.cwbl_last_error()
             raise CwblError(f"{ERRORS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+    def set_stream(self, stream):
+        """Order device-memory calls after the work queued on `stream` (a torch.cuda.Stream,
+        a raw hipStream_t as int, or None for the legacy null stream)."""
+        raw = getattr(stream, "cuda_stream", stream)
+        self._check(self.lib.cwbl_set_stream(raw or None))
 
     def set_obs(self, obs_set):
         self._check(self.lib.cwbl_set_obs(C.byref(obs_set)))

@@ -65,11 +65,14 @@ def radar_var_params(hclr, vclr, max_lz, err, err_rej, radar_type, multi_infl=1.
                           rtps_alpha=0.95, radar={radar_type: tp})
 
 
-def make(name="c2", seed=20261015, scale=None, shard=None, **over):
+def make(name="c2", seed=20261015, scale=None, shard=None, local_noise=False, **over):
     """Build a workload.  `scale` shrinks nx/ny (domain and obs count scale with it) for
     tests; `shard` = (rank, world) keeps that rank's columns of the reference's cyclic
     block-1 column grid (letkf_local_info, module_mpi_util.f90:71-188; dist.shard_columns).
-    The obs set never depends on `shard`."""
+    The obs set never depends on `shard`.  `local_noise` (with `shard`): draw the members'
+    noise for the shard's columns only, from a per-rank stream (the bench's large grids: a
+    rank never materialises the whole ensemble; the values then differ from the unsharded
+    workload's, the obs set and the geometry do not)."""
     cfg = dict(CONFIGS[name])
     cfg.update(over)
     if scale:
@@ -92,13 +95,19 @@ def make(name="c2", seed=20261015, scale=None, shard=None, **over):
     # grid: 2 km spacing, 50 levels 0..20 km with small column-dependent jitter
     jx = np.arange(nx, dtype=np.float64) * dx
     jy = np.arange(ny, dtype=np.float64) * dx
+    if shard is not None and local_noise:
+        from .dist import shard_columns
+        xs, ys = shard_columns(nx, ny, shard[0], shard[1])
+        jx, jy = jx[xs], jy[ys]
+        rng = np.random.default_rng([seed, shard[0], shard[1]])
+        shard = None
     X, Y = np.meshgrid(jx, jy)                        # (ny, nx)
     lev = np.linspace(20.0, 20e3, nz)
     alt = (lev[:, None, None] + 15.0 * np.sin(X / 9e3)[None] * np.cos(Y / 11e3)[None]).astype(np.float32)
     tr = _truth(X[None].astype(np.float32), Y[None].astype(np.float32), alt)  # (nz,ny,nx)
-    var = np.empty((k, nz, ny, nx), np.float32)
+    var = np.empty((k,) + tr.shape, np.float32)
     for m in range(k):
-        var[m] = tr + rng.standard_normal((nz, ny, nx), dtype=np.float32)
+        var[m] = tr + rng.standard_normal(tr.shape, dtype=np.float32)
     x = X.astype(np.float32)
     y = Y.astype(np.float32)
     if shard is not None:

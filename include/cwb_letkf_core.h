@@ -74,7 +74,7 @@ enum {
   CWBL_ERR_STATE = 2,        /* call order (e.g. analyze before init/set_obs)    */
   CWBL_ERR_NO_DEVICE = 3,    /* no HIP device / wrong architecture              */
   CWBL_ERR_HIP = 4,          /* HIP runtime error                               */
-  CWBL_ERR_UNSUPPORTED = 5,  /* configuration outside v1 (e.g. k > 64)          */
+  CWBL_ERR_UNSUPPORTED = 5,  /* configuration outside this build (e.g. k > 128)  */
   CWBL_ERR_OOM = 6
 };
 
@@ -188,13 +188,20 @@ typedef struct cwbl_stats {
 } cwbl_stats;
 
 int         cwbl_init(const cwbl_init_params *params);
+/* Device-memory calls (CWBL_MEM_DEVICE and the transpose helpers) are ordered after the work
+ * queued so far on the caller's stream: an event recorded there, waited on by the library's
+ * own streams.  `stream` is a hipStream_t (NULL = the legacy null stream, the default).  No
+ * reference counterpart: the reference has no device (its arrays are complete on entry). */
+int         cwbl_set_stream(void *stream);
 int         cwbl_set_obs(const cwbl_obs_set *obs);
 int         cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *slab,
                              cwbl_stats *stats /* nullable */);
 
-/* letkf_solve for npts points.  Point i uses columns [col_off[i], col_off[i+1]) of
- * yo(ncol) and yb(k,ncol) (member fastest), xb(k,npts) -> xa(k,npts).  evals (nullable)
- * receives the eigenvalues of inflat*I + yb yb^T per point, ascending (k,npts). */
+/* letkf_solve for npts points (module_letkf_core.f90:598-700).  Point i uses columns
+ * [col_off[i], col_off[i+1]) of yo(ncol) and yb(k,ncol) (member fastest), xb(k,npts) ->
+ * xa(k,npts).  evals (nullable) receives the eigenvalues of inflat*I + yb yb^T per point in
+ * ascending order (k,npts), as dsyevd returns them in inverse_matrix (module_eigen.f90:48-49;
+ * the reference keeps 1/lambda in eigen::eval afterwards), at every k <= 128. */
 int         cwbl_solve_batch(int npts, const long long *col_off, const float *yo,
                              const float *yb, const float *xb, float inflat,
                              int use_rtpp, float rtpp_alpha, int use_rtps, float rtps_alpha,

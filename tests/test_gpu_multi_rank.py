@@ -1,0 +1,95 @@
+"""The sharded path with the HIP core in every rank (world size 2, one GPU, gloo transport).
+
+What bench.py --gpus N and the reference's flat-MPI layout do (module_mpi_util.f90:38-56,
+73-188): grid columns dealt over a px x py cyclic block-1 rank grid, the obs set packed on
+rank 0 and broadcast once (cwbl/dist.py broadcast_obs_set, the device buffer of the wire
+format) and handed to the core as DEVICE memory (builder_from(MEM_DEVICE)), each rank
+analysing its own columns with cwbl_analyze_var.  Both ranks share cuda:0 (RCCL refuses two
+ranks per device; gloo carries the broadcast of the device buffer).  The reassembled output
+must equal the single-process HIP analysis of the whole grid bit for bit, and the oracle
+within the north_star tolerance.
+"""
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cwbl import abi, synth
+from cwbl import dist as cdist
+from helpers import increment_rel_rms, oracle
+
+pytestmark = pytest.mark.gpu
+
+INCR_TOL = 1e-6
+CASE = dict(name="c2", seed=23, scale=0.1, nz=10)  # 30 x 30 x 10, k = 40
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    c = dict(CASE)
+    w = synth.make(c.pop("name"), shard=(rank, world), **c)
+    types = None
+    if rank == 0:
+        types = [dict(family=1, type_id=w.radar_type, xyz=w.obs_xyz, obs=w.obs, hdxb=w.hdxb)]
+    k, got = cdist.broadcast_obs_set(types, w.k, dev, src=0)
+    assert k == w.k and got[0]["xyz"].is_cuda
+    core = abi.Core(k, device=0)
+    core.set_obs(cdist.builder_from(got, abi.MEM_DEVICE).build())
+    x, y, alt, var = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt, w.var))
+    st = core.analyze_var(w.vp, abi.make_slab(x, y, alt, var, memory=abi.MEM_DEVICE))
+    np.save(os.path.join(out_dir, f"rank{rank}.npy"), var.cpu().numpy())
+    np.save(os.path.join(out_dir, f"stats{rank}.npy"),
+            np.array([st.points, st.solved, st.nobs_sum, st.nonconverged], np.int64))
+    core.finalize()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_hip_core_equals_single_process_and_oracle(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    c = dict(CASE)
+    full = synth.make(c.pop("name"), **c)
+    # the single-process HIP analysis of the whole grid (host-memory slab)
+    core = abi.Core(full.k, device=0)
+    core.set_obs(abi.ObsSetBuilder().add_radar(full.radar_type, full.obs_xyz, full.obs,
+                                               full.hdxb).build())
+    one = full.var.copy()
+    st1 = core.analyze_var(full.vp, abi.make_slab(full.x, full.y, full.alt, one))
+    core.finalize()
+    got = np.empty_like(one)
+    seen = np.zeros(one.shape[2:], np.int32)
+    tot = np.zeros(4, np.int64)
+    for r in range(world):
+        xs, ys = cdist.shard_columns(full.nx, full.ny, r, world)
+        got[:, :, ys[:, None], xs[None, :]] = np.load(tmp_path / f"rank{r}.npy")
+        seen[ys[:, None], xs[None, :]] += 1
+        tot += np.load(tmp_path / f"stats{r}.npy")
+    assert (seen == 1).all()
+    assert tot[0] == st1.points and tot[1] == st1.solved and tot[2] == st1.nobs_sum
+    assert tot[3] == 0 and st1.solved > 0
+    np.testing.assert_array_equal(got.view(np.uint32), one.view(np.uint32))
+    ref = full.var.copy()
+    ob = abi.ObsSetBuilder().add_radar(full.radar_type, full.obs_xyz, full.obs, full.hdxb).build()
+    rc = oracle().orc_analyze_var(full.k, 0, -5.0, 0, C.byref(ob), C.byref(full.vp),
+                                  C.byref(abi.make_slab(full.x, full.y, full.alt, ref)), 16,
+                                  C.byref(abi.Stats()))
+    assert rc == 0
+    rel = increment_rel_rms(got, ref, full.var)
+    assert rel <= INCR_TOL, rel

@@ -32,10 +32,17 @@ def core(k, wf=0, norain=-5.0, q1=abi.Q1_REPLICATE):
     return _cores["core"]
 
 
-@pytest.mark.parametrize("k", [8, 40, 64])
-def test_solve_batch_matches_reference(k):
+@pytest.mark.parametrize("k,solver", [(8, "tq"), (40, "tq"), (64, "tq"), (128, "tq"),
+                                      (8, "jacobi"), (40, "jacobi"), (64, "jacobi")])
+def test_solve_batch_matches_reference(k, solver, monkeypatch):
+    """G1 through cwbl_solve_batch with the eigenvalue output: increments within 1e-6 and
+    dsyevd's ascending eigenvalues within 1e-12 at every k.  Default: the tq kernels' T and
+    bisection (cwbl_eig.hip); CWBL_SOLVER=jacobi (k <= 64): the Jacobi eigensolver."""
     g = golden(f"solve_k{k}.npz")
-    c = core(k)
+    if solver == "jacobi":
+        monkeypatch.setenv("CWBL_SOLVER", "jacobi")
+    _cores.clear()
+    c = abi.Core(k, device=0)
     col = g["col_off"]
     # group points that share the solve parameters
     keys = list(zip(g["multi_infl"], g["use_rtpp"], g["use_rtps"], g["rtpp_alpha"], g["rtps_alpha"]))
@@ -53,8 +60,38 @@ def test_solve_batch_matches_reference(k):
             worst = max(worst, increment_rel_rms(xa[n], g["xa"][i], g["xb"][i]))
             rel = np.max(np.abs(ev[n] - g["lam"][i]) / np.abs(g["lam"][i]))
             worst_eig = max(worst_eig, rel)
+    c.finalize()
     assert worst <= INCR_TOL, worst
     assert worst_eig <= EIG_TOL, worst_eig
+
+
+@pytest.mark.parametrize("k", [2, 3, 9, 25, 33, 65, 97, 128])
+def test_eigenvalues_at_every_padding_class(k):
+    """Random batches at k's of every kernel class (KP = 8..64 one wavefront, k = 25..32 at
+    KP = 40, KP = 96 and 128 on 256 threads), including points with p < k (k - p equal
+    eigenvalues inflat), p = 0 and tiny p: ascending eigenvalues within 1e-12 of the
+    oracle's dsyevd."""
+    from helpers import oracle_solve
+    rng = np.random.default_rng(k)
+    ps = [0, 1, 2, k - 1, k, k + 3, 200][: 7 if k > 2 else 6]
+    ps = [p for p in ps if p >= 0]
+    col = np.concatenate([[0], np.cumsum(ps)]).astype(np.int64)
+    yo = rng.standard_normal(col[-1]).astype(np.float32)
+    yb = (rng.standard_normal((col[-1], k)) * rng.uniform(0.1, 3.0, (col[-1], 1))).astype(np.float32)
+    xb = (280.0 + rng.standard_normal((len(ps), k))).astype(np.float32)
+    infl = inflat_of(k, 1.6)
+    c = core(k)
+    xa, ev = c.solve_batch(col, yo, yb.ravel(), xb, infl, 1, 0.95, 1, 0.95, want_evals=True)
+    for i, p in enumerate(ps):
+        assert np.all(np.diff(ev[i]) >= 0), (p, ev[i])
+        if p == 0:
+            np.testing.assert_allclose(ev[i], np.float64(infl), rtol=4e-16, atol=0)
+            np.testing.assert_array_equal(xa[i], xb[i])
+            continue
+        xr, lr = oracle_solve(k, p, xb[i], yo[col[i]:col[i + 1]], yb[col[i]:col[i + 1]], infl,
+                              1, 0.95, 1, 0.95)
+        assert np.max(np.abs(ev[i] - lr) / np.abs(lr)) <= EIG_TOL, (p, ev[i] - lr)
+        assert increment_rel_rms(xa[i], xr, xb[i]) <= INCR_TOL
 
 
 @pytest.mark.parametrize("k", [8, 40, 64, 128])
@@ -76,18 +113,11 @@ def test_solve_batch_tq_matches_reference(k):
 
 
 def test_k_limits():
-    """k up to 128 is supported (k > 64 on the 256-thread kernel); beyond that, and the
-    eigenvalue output above k = 64 (the Jacobi path), report UNSUPPORTED."""
+    """k up to 128 is supported (k > 64 on the 256-thread kernels); beyond that the library
+    reports UNSUPPORTED."""
     with pytest.raises(abi.CwblError, match="UNSUPPORTED"):
         abi.Core(129, device=0)
     _cores.clear()
-    c = core(128)
-    g = golden("solve_k128.npz")
-    col = g["col_off"]
-    off = np.array([0, col[1] - col[0]], np.int64)
-    with pytest.raises(abi.CwblError, match="UNSUPPORTED"):
-        c.solve_batch(off, g["yo"][col[0]:col[1]], g["yb"][:col[1] * 128], g["xb"][0][None],
-                      inflat_of(128, g["multi_infl"][0]), 1, 0.95, 1, 0.95, want_evals=True)
 
 
 SEARCHES = ["search_3d.npz", "search_3d_overflow.npz", "search_2d.npz",
@@ -147,14 +177,18 @@ def test_device_memory_path_equals_host_path():
     np.testing.assert_array_equal(got.view(np.uint32), hvar.view(np.uint32))
 
 
-def test_device_inputs_only_need_to_be_queued():
+@pytest.mark.parametrize("where", ["side_stream", "default_stream"])
+def test_device_inputs_only_need_to_be_queued(where):
     """cwbl_set_obs / cwbl_analyze_var on device buffers whose producers are still queued
-    (behind a GPU spin on a side stream): the library orders itself after them."""
+    (behind a GPU spin) on the caller's stream: a side stream declared with cwbl_set_stream,
+    or torch's default (legacy null) stream, the library's default.  The library orders
+    itself after that stream's queued work by an event (not a device-wide synchronise)."""
     torch = pytest.importorskip("torch")
     case = DriverCase("driver_mixed.npz")
     c = core(case.k, case.wf, case.norain)
     dev = torch.device("cuda:0")
-    s = torch.cuda.Stream()
+    s = torch.cuda.Stream() if where == "side_stream" else torch.cuda.default_stream()
+    c.set_stream(s)
     staged = []
 
     def late(a):  # a device copy of `a` written only after ~10 ms of GPU spin on stream s
@@ -172,6 +206,7 @@ def test_device_inputs_only_need_to_be_queued():
     var = late(np.asarray(case.var_in, np.float32).copy())
     slab = abi.make_slab(x, y, alt, var, case.ix_lim, case.iy_lim, memory=abi.MEM_DEVICE)
     c.analyze_var(case.vp, slab)
+    c.set_stream(None)
     got = var.cpu().numpy()
     c.set_obs(case.obs_set())
     hslab, hvar = case.slab()
@@ -218,16 +253,15 @@ def test_synthetic_c2_subdomain_vs_oracle():
 @pytest.mark.parametrize("k", [25, 32, 33, 36, 40])
 def test_split_kp40_path_vs_one_kernel_and_oracle(k, monkeypatch):
     """The KP = 40 slab path runs split by default (assemble_record_kernel writes A and Yb d,
-    solve_tq40_kernel runs the whole tridiagonalisation four points per wavefront, CWBL_TQ4=1);
-    CWBL_TQ4=8 is the earlier split (solve_tq_kernel<40, false, 8> hands the trailing 32x32
-    matrix to solve_tq4_kernel).  k < 40 exercises the identity padding (the no-op steps past
+    solve_tq40_kernel runs the whole tridiagonalisation four points per wavefront, CWBL_TQ4=1).
+    k < 40 exercises the identity padding (the no-op steps past
     k - 2); k = 25..32 run at KP = 40 too (their one-kernel path, CWBL_TQ4=0, is KP = 32).
     Both against the one-kernel path (CWBL_TQ4=0) and the oracle on a 30x30x50 C2-shaped
     grid."""
     import ctypes as C
     w = _radar_case_scaled(0.1, k=k)
     out = {}
-    for mode in ("0", "1", "8"):
+    for mode in ("0", "1"):
         monkeypatch.setenv("CWBL_TQ4", mode)
         _cores.clear()
         c = abi.Core(w.k, device=0)
@@ -237,19 +271,18 @@ def test_split_kp40_path_vs_one_kernel_and_oracle(k, monkeypatch):
         c.finalize()
         assert st.nonconverged == 0 and st.solved > 0
         out[mode] = (var, st.solved, st.nobs_sum)
-    assert out["0"][1:] == out["1"][1:] == out["8"][1:]
+    assert out["0"][1:] == out["1"][1:]
     ref = w.var.copy()
     ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
     rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
                                   C.byref(abi.make_slab(w.x, w.y, w.alt, ref)), 16,
                                   C.byref(abi.Stats()))
     assert rc == 0
-    for mode in ("0", "1", "8"):
+    for mode in ("0", "1"):
         rel = increment_rel_rms(out[mode][0], ref, w.var)
         assert rel <= INCR_TOL, (mode, rel)
-    for mode in ("1", "8"):
-        rel = increment_rel_rms(out[mode][0], out["0"][0], w.var)
-        assert rel <= INCR_TOL, (mode, rel)
+    rel = increment_rel_rms(out["1"][0], out["0"][0], w.var)
+    assert rel <= INCR_TOL, rel
 
 
 @pytest.mark.parametrize("n_obs", [40, 120])
@@ -671,3 +704,62 @@ def test_binned_search_equals_tree_search(name, monkeypatch):
         assert out["bins"][3] > 0  # the fallback ran
     rel = increment_rel_rms(out["bins"][0], out["tree"][0], var_in)
     assert rel <= 1e-9, rel
+
+
+def _pair_ensemble(w, err, seed=5):
+    """Replace a synthetic workload's values by a member-pair ensemble on a dyadic grid
+    (members 2i, 2i+1 = mean +/- delta_i, k a power of two): the fp32 means are exact, so the
+    perturbations are exactly zero-sum (in the reference too, module_letkf_core.f90:430-434,
+    671).  The (k/2)-dimensional pair-symmetric subspace then carries eigenvalue inflat exactly
+    and no part of x' or Yb d, so the problem stays well posed when tiny obs errors push the
+    spectrum bound M/m far past 1e12: the reference's dsyevd path and the quadrature agree
+    there, instead of both resolving an ill-conditioned direction to O(kappa eps)."""
+    rng = np.random.default_rng(seed)
+    k, n = w.k, w.obs.shape[0]
+    dy = lambda a: (np.round(np.asarray(a) * 256.0) / 256.0).astype(np.float32)  # noqa: E731
+    sgn = np.where(np.arange(k) % 2 == 0, 1.0, -1.0)[:, None]
+    mu = dy(rng.standard_normal(n))
+    delta = dy(2.0 * rng.standard_normal((k // 2, n)))
+    w.hdxb = dy(mu[None, :] + sgn * np.repeat(delta, 2, axis=0))
+    w.obs = dy(mu + rng.standard_normal(n))
+    shape = w.var.shape[1:]
+    xm = dy(rng.standard_normal(shape))
+    eps = dy(rng.standard_normal((k // 2,) + shape))
+    w.var = np.ascontiguousarray(dy(xm[None] + sgn.reshape((k, 1, 1, 1)) * np.repeat(eps, 2, axis=0)))
+    from cwbl import synth
+    cfg = w.extra["cfg"]
+    w.vp = synth.radar_var_params(cfg["hclr"], cfg["vclr"], cfg["max_lz"], err, cfg["err_rej"],
+                                  w.radar_type)
+    # RTPS off: with every direction observed this precisely the analysis spread is ~1e-7 of
+    # the background's, so the reference's fp32 xa' = xa - mean(xa) (:684-697) is pure
+    # rounding, and RTPS would rescale that rounding by ~1e7 (RTPP keeps alpha xb')
+    w.vp.use_rtps = 0
+    return w
+
+
+@pytest.mark.parametrize("k,err", [(32, 2.0 ** -20), (32, 2.0 ** -30), (16, 2.0 ** -20),
+                                   (64, 2.0 ** -20), (128, 2.0 ** -20), (128, 2.0 ** -30)])
+def test_tiny_obs_errors_beyond_the_31_node_rule(k, err):
+    """Obs errors of 2^-20 and 2^-30 put trace(A)/m far above 1e12 (decades 13..24): the
+    kernels switch to the 63-node rule (solve_tq40_kernel: 8 rounds; the one-wavefront kernels
+    and the 256-thread/tail pair: a second pass), where before round 3 such points were only
+    counted as non-converged.  k = 32 runs the KP = 40 record path, 16 and 64 solve_tq_kernel,
+    128 the split big path; all against the oracle (the reference's dsyevd path)."""
+    import ctypes as C
+    from cwbl import synth
+    w = _pair_ensemble(synth.make("c2", seed=13, scale=0.06, nz=4, k=k), err)
+    c = core(k)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    var = w.var.copy()
+    st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+    ref = w.var.copy()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    ost = abi.Stats()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(w.x, w.y, w.alt, ref)), 16, C.byref(ost))
+    assert rc == 0
+    assert st.solved == ost.solved > 0 and st.nobs_sum == ost.nobs_sum
+    assert st.max_sweeps > 12, st.max_sweeps          # the decade of the spectrum bound
+    assert st.nonconverged == 0
+    rel = increment_rel_rms(var, ref, w.var)
+    assert rel <= INCR_TOL, rel

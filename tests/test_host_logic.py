@@ -77,3 +77,30 @@ def test_make_slab_rejects_arrays_the_abi_would_misread():
     abi.ObsSetBuilder().add_gts(abi.GTS_SYNOP, np.zeros((2, 3)), np.zeros((2, 5)),
                                 np.ones((2, 5)), np.zeros((k, 2, 5)),
                                 np.zeros((k, 2, 5), np.int64)).build()
+
+
+def test_local_noise_shards_keep_the_geometry():
+    full = synth.make("c2", scale=0.05, nz=3)
+    for world in (2, 4):
+        from cwbl.dist import shard_columns
+        for r in range(world):
+            part = synth.make("c2", scale=0.05, nz=3, shard=(r, world), local_noise=True)
+            xs, ys = shard_columns(full.nx, full.ny, r, world)
+            np.testing.assert_array_equal(part.x, full.x[np.ix_(ys, xs)])
+            np.testing.assert_array_equal(part.alt, full.alt[:, ys][:, :, xs])
+            np.testing.assert_array_equal(part.obs_xyz, full.obs_xyz)
+            assert part.var.shape == (40, 3, len(ys), len(xs))
+
+
+def test_bench_refuses_a_rank_count_that_is_not_gpus():
+    """bench.py --gpus N must time N ranks: under a launcher whose WORLD_SIZE differs it
+    exits non-zero before touching the GPU (--gpus was ignored)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, r.stderr
+    assert "--gpus 2 but WORLD_SIZE=1" in r.stderr
