@@ -395,6 +395,12 @@ SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps,
 }
 
 }  // namespace
+
+int set_last_error(int code, const char *msg) {
+  g_err = msg;
+  return code;
+}
+
 }  // namespace cwbl
 
 using namespace cwbl;

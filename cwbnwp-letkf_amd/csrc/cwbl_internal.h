@@ -291,6 +291,8 @@ __host__ __device__ inline unsigned list_slot(int s) {
 }
 
 int supported_kp(int k);      // smallest compiled KP >= k, or -1
+// sets the message cwbl_last_error() returns and returns `code` (cwbl_abi.hip)
+int set_last_error(int code, const char *msg);
 constexpr int kMaxWaveKP = 64;  // largest KP of the one-wavefront kernels
 
 }  // namespace cwbl

@@ -9,7 +9,9 @@
 ! line for line, with the file:line it follows.
 !
 ! Usage: ref_harness <mode> <in.bin> <out.bin>,
-! modes: consts | solve | search | gc | driver | tuneq
+! modes: consts | solve | search | gc | driver | tuneq | ingest
+! (ingest also compiles module_projection and the source text of the obs readers
+! read_gts_omboma / read_alt_info / get_alt / read_radar; see build_ref.sh)
 ! All files are unformatted stream (little-endian int32 / real32 / real64).
 module harness_lib
     use param
@@ -17,6 +19,8 @@ module harness_lib
     use eigen
     use kdtree2_module
     use ref_extract
+    use projection, only : proj_type
+    use ref_ingest
     implicit none
 
     character(len=512) :: fin, fout
@@ -193,6 +197,81 @@ contains
         close(21)
     end subroutine do_tuneq
 
+    ! Obs readers and projection KATs (module_gts_omboma.f90:48-506,704-1049,
+    ! module_radar.f90:30-118, module_projection.f90:21-50), run in the directory that holds
+    ! the files, as cwb_letkf.f90:46-52 names them: member m (1-based) reads gts_letkf_mmm
+    ! with obs_gts, and VR_/MR_/MD_/MK_letkf_mmm; projection_nml at its defaults
+    ! (module_config.f90:70-75).  The distribution (gts_distribute / radar_distribute) takes
+    ! every array but hdxb / qc from the root reader, member 1 (cwb_letkf.f90:46-57), and
+    ! member m's hdxb(:,:,m-1) / qc(:,:,m-1) from member m's reader.
+    ! in:  k, n (i4), has(5) (i4: gts, VR, MR, MD, MK), lon(n), lat(n) (r4)
+    ! out: xy(2,n) (r4); per GTS type with nobs > 0: type, nvar, nobs (i4), id (5 chars each),
+    !      lat, lon, alt (nobs), xyz(3,nobs), obs(nvar,nobs), error(nvar,nobs) (r4), then per
+    !      member hdxb(nvar,nobs) (r4), then per member qc(nvar,nobs) (i4); 0 (i4); per radar
+    !      type with nobs > 0: type, nobs, obs, lat, lon, alt, xyz(3,nobs), per member
+    !      hdxb(nobs); 0
+    subroutine do_ingest
+        integer :: k, n, has(5), m, t, i
+        real, allocatable :: lon(:), lat(:)
+        real :: xy(2)
+        character(len=3) :: proc
+        type(proj_type) :: proj
+        type(wrfda_gts), allocatable :: g(:)
+        type(cwb_radar), allocatable :: r(:)
+        character(len=2), parameter :: rnames(4) = (/ 'MR', 'VR', 'MD', 'MK' /)
+        integer, parameter :: rflag(4) = (/ 3, 2, 4, 5 /)    ! dbz, vr, zdr, kdp -> has()
+        open(40, file=trim(fin), access='stream', form='unformatted', status='old')
+        read(40) k, n
+        read(40) has
+        allocate(lon(n), lat(n))
+        read(40) lon, lat
+        close(40)
+        call setup_k(k)
+        call proj % init()
+        open(21, file=trim(fout), access='stream', form='unformatted', status='replace')
+        do i = 1, n
+            xy = proj % lonlat_to_xy(lon(i), lat(i))
+            write(21) xy
+        end do
+        allocate(g(k), r(k))
+        do m = 1, k
+            allocate(g(m) % platform(num_gts_indexes), r(m) % radarobs(num_radar_indexes))
+            write(proc, '(i3.3)') m
+            if (has(1) /= 0) call read_gts_omboma(g(m), proj, 'gts_letkf_'//proc, 'obs_gts')
+            do t = 1, num_radar_indexes
+                if (has(rflag(t)) /= 0) &
+                    call read_radar(r(m), proj, rnames(t)//'_letkf_'//proc, rnames(t))
+            end do
+        end do
+        do t = 1, num_gts_indexes
+            associate (p => g(1) % platform(t))
+                if (p % nobs <= 0) cycle
+                write(21) t, size(p % obs, 1), p % nobs
+                write(21) p % id
+                write(21) p % lat, p % lon, p % alt, p % xyz, p % obs, p % error
+                do m = 1, k
+                    write(21) g(m) % platform(t) % hdxb(:, :, m-1)
+                end do
+                do m = 1, k
+                    write(21) g(m) % platform(t) % qc(:, :, m-1)
+                end do
+            end associate
+        end do
+        write(21) 0
+        do t = 1, num_radar_indexes
+            associate (p => r(1) % radarobs(t))
+                if (p % nobs <= 0) cycle
+                write(21) t, p % nobs
+                write(21) p % obs, p % lat, p % lon, p % alt, p % xyz
+                do m = 1, k
+                    write(21) r(m) % radarobs(t) % hdxb(:, m-1)
+                end do
+            end associate
+        end do
+        write(21) 0
+        close(21)
+    end subroutine do_ingest
+
     include 'ref_driver.inc'
 
 end module harness_lib
@@ -219,6 +298,8 @@ program ref_harness
         call do_driver
     case ('tuneq')
         call do_tuneq
+    case ('ingest')
+        call do_ingest
     case default
         stop "ref_harness: unknown mode"
     end select

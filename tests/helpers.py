@@ -129,3 +129,121 @@ def increment_rel_rms(xa, xa_ref, xb):
     den = np.sqrt(np.mean((xa_ref[fin] - xb[fin]) ** 2)) if fin.any() else 0.0
     num = np.sqrt(np.mean((xa[fin] - xa_ref[fin]) ** 2)) if fin.any() else 0.0
     return num / den if den > 0 else num
+
+
+# ---- an independent fp64 evaluation of letkf_solve for ill-conditioned spectra ---------------
+def eigen_direct_solve(k, xb, yo, yb, inflat, rp, ra, sp, sa):
+    """letkf_solve (module_letkf_core.f90:598-700) with the eigendecomposition applied to the
+    two vectors directly: wbar . x' = sum_a (q_a . Yb d)(q_a . x') / lam_a and
+    W x' = sqrt(k-1) sum_a q_a (q_a . x') / sqrt(lam_a), never forming Pa = V L^-1 V^T.
+    The reference forms Pa (dgemm) and multiplies it by Yb d; when tiny obs errors make
+    |Yb d| ~ 1e13 the rounding of Pa's entries alone (~1e-17) moves wbar by ~1e-4 (measured
+    against 60-digit arithmetic: scratch work), whereas here both factors of
+    the ill-conditioned directions are small.  fp32 inputs and the fp32 epilogue follow the
+    reference's order (oracle/letkf_oracle.c:506-541).  yb: (p, k) member fastest."""
+    yb8 = np.asarray(yb, np.float64).reshape(-1, k)
+    A = yb8.T @ yb8 + float(np.float32(inflat)) * np.eye(k)
+    lam, Q = np.linalg.eigh(A)
+    # A = inflat I + Yb Yb^T >= inflat: where |A| ~ 1e14 the computed eigenvalues of the
+    # unobserved directions scatter by eps |A| around inflat (x' and Yb d have no part there)
+    lam = np.maximum(lam, float(np.float32(inflat)))
+    yd = yb8.T @ np.asarray(yo, np.float64)
+    xb = np.asarray(xb, np.float32)
+    s = np.float32(0.0)
+    for v in xb:
+        s = np.float32(s + v)
+    xb_mean = float(np.float32(s * np.float32(1.0 / k)))
+    xp = xb.astype(np.float64) - xb_mean
+    cx = Q.T @ xp
+    dot = float(np.sum((Q.T @ yd) * cx / lam))
+    wx = np.sqrt(k - 1.0) * (Q @ (cx / np.sqrt(lam)))
+    xa = (xb_mean + (dot + wx)).astype(np.float32)
+    if rp or sp:
+        ninv = np.float32(1.0 / k)
+        s = np.float32(0.0)
+        for v in xa:
+            s = np.float32(s + v)
+        xa_mean = np.float32(s * ninv)
+        xap = (xa - xa_mean).astype(np.float32)
+        if rp:
+            a1 = np.float32(np.float32(1.0) - np.float32(ra))
+            xap = ((a1 * xap).astype(np.float64) + float(np.float32(ra)) * xp).astype(np.float32)
+        if sp:
+            d8 = 0.0
+            for v in xp:
+                d8 = d8 + v * v
+            xa_std = np.float32(0.0)
+            for v in xap:
+                xa_std = np.float32(xa_std + v * v)
+            a = np.float32(sa)
+            fac = np.float32(a * np.sqrt(np.float32(np.float32(d8) / xa_std)) - a + np.float32(1.0))
+            xap = (xap * fac).astype(np.float32)
+        xa = (xa_mean + xap).astype(np.float32)
+    return xa
+
+
+def radar_point_columns(w, kz, j, i, err):
+    """letkf_yoyb's columns (module_letkf_core.f90:478-523) of grid point (kz, j, i) for a
+    one-radar-type workload with Gaussian weights and no max_lz_pts truncation: the obs within
+    the fixed ball (fp32 distances as kdtree2 computes them), reference fp32 order, the
+    oracle's expf (glibc's).  Returns (yo (p,), yb (p, k)); the column order is obs-index
+    order, not kdtree2's, which changes only the order of fp64 sums."""
+    lib = oracle()
+    k = w.k
+    cfg = w.extra["cfg"]
+    f = np.float32
+    hinv, vinv = f(1.0) / f(f(cfg["hclr"]) * f(1e3)), f(1.0) / f(f(cfg["vclr"]) * f(1e3))
+    on = np.stack([w.obs_xyz[:, 0] * hinv, w.obs_xyz[:, 1] * hinv, w.obs_xyz[:, 2] * vinv], 1)
+    q = np.array([w.x[j, i] * hinv, w.y[j, i] * hinv, w.alt[kz, j, i] * vinv], np.float32)
+    d = (on - q).astype(np.float32)
+    r2 = ((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]).astype(np.float32) + d[:, 2] * d[:, 2]).astype(np.float32)
+    sel = np.where(r2 <= lib.orc_search_r2())[0]
+    hd = w.hdxb[:, sel]
+    s = np.zeros(len(sel), np.float32)
+    for m in range(k):
+        s = (s + hd[m]).astype(np.float32)
+    mean = (s * f(1.0 / k)).astype(np.float32)
+    bg = (hd - mean).astype(np.float32)
+    dd = np.zeros(len(sel), np.float32)
+    for m in range(k):
+        dd = (dd + bg[m] * bg[m]).astype(np.float32)
+    omm = (w.obs[sel] - mean).astype(np.float32)
+    std = np.sqrt((dd * f(1.0 / (k - 1))).astype(np.float32))
+    e = f(err)
+    rej = f(w.vp.radar[w.radar_type - 1].err_rej[0])
+    keep = ~(np.abs(omm) > (np.sqrt((std * std + e * e).astype(np.float32)) * rej).astype(np.float32))
+    einv = np.array([f(1.0) / f(e * f(lib.orc_expf(f(0.25) * v))) for v in r2[sel]], np.float32)
+    yo = (omm * einv).astype(np.float32)[keep]
+    yb = (bg * einv).astype(np.float32).T[keep]
+    return yo, yb
+
+
+def pair_ensemble(w, err, seed=5):
+    """Replace a synthetic workload's values by a member-pair ensemble on a dyadic grid
+    (members 2i, 2i+1 = mean +/- delta_i, k a power of two): the fp32 means are exact, so the
+    perturbations are exactly zero-sum (in the reference too, module_letkf_core.f90:430-434,
+    671).  The (k/2)-dimensional pair-symmetric subspace then carries eigenvalue inflat exactly
+    and no part of x' or Yb d, so the problem stays well posed when tiny obs errors push the
+    spectrum bound M/m far past 1e12: the reference's dsyevd path and the quadrature agree
+    there, instead of both resolving an ill-conditioned direction to O(kappa eps)."""
+    rng = np.random.default_rng(seed)
+    k, n = w.k, w.obs.shape[0]
+    dy = lambda a: (np.round(np.asarray(a) * 256.0) / 256.0).astype(np.float32)  # noqa: E731
+    sgn = np.where(np.arange(k) % 2 == 0, 1.0, -1.0)[:, None]
+    mu = dy(rng.standard_normal(n))
+    delta = dy(2.0 * rng.standard_normal((k // 2, n)))
+    w.hdxb = dy(mu[None, :] + sgn * np.repeat(delta, 2, axis=0))
+    w.obs = dy(mu + rng.standard_normal(n))
+    shape = w.var.shape[1:]
+    xm = dy(rng.standard_normal(shape))
+    eps = dy(rng.standard_normal((k // 2,) + shape))
+    w.var = np.ascontiguousarray(dy(xm[None] + sgn.reshape((k, 1, 1, 1)) * np.repeat(eps, 2, axis=0)))
+    from cwbl import synth
+    cfg = w.extra["cfg"]
+    w.vp = synth.radar_var_params(cfg["hclr"], cfg["vclr"], cfg["max_lz"], err, cfg["err_rej"],
+                                  w.radar_type)
+    # RTPS off: with every direction observed this precisely the analysis spread is ~1e-7 of
+    # the background's, so the reference's fp32 xa' = xa - mean(xa) (:684-697) is pure
+    # rounding, and RTPS would rescale that rounding by ~1e7 (RTPP keeps alpha xb')
+    w.vp.use_rtps = 0
+    return w
