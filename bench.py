@@ -485,7 +485,7 @@ def main():
         # the host's rule (cwbl_analyze_var): KP = 96 / 128 split after kp - 64 steps when
         # k > kp - 62, unless CWBL_BIG_SPLIT=0
         split_big = kp in (96, 128) and k > kp - 62 and os.environ.get("CWBL_BIG_SPLIT", "1") != "0"
-        kpair = ("assemble_record_kernel<40, 4>", "solve_tq40_kernel<40, 0>")
+        kpair = ("assemble_record_kernel<4>", "solve_tq40_kernel<40, 0>")
         kname = (" + ".join(kpair) if split else
                  f"solve_tq_big_kernel<{kp}, false, {kp - 64}> + "
                  f"solve_tqb_tail_kernel<{kp}, {kp - 64}, 2>" if split_big else

@@ -129,6 +129,7 @@ struct State {
   bool big_split = true;                              // CWBL_BIG_SPLIT=0: one-kernel KP=128 solve
   long long big_sub = 32768;                          // CWBL_BIG_SUB: KP=128 hand-off batch
   std::vector<hipEvent_t> events;
+  hipStream_t h2d = nullptr, d2h = nullptr;           // host-memory slab copies (pipelined)
   hipStream_t caller_stream = nullptr;                // cwbl_set_stream (null: legacy stream)
   hipEvent_t order_ev = nullptr;                      // order_after_caller
 };
@@ -369,6 +370,10 @@ void release_all() {
   S.stream = nullptr;
   if (S.sstream) (void)hipStreamDestroy(S.sstream);
   S.sstream = nullptr;
+  for (hipStream_t *st : {&S.h2d, &S.d2h}) {
+    if (*st) (void)hipStreamDestroy(*st);
+    *st = nullptr;
+  }
   S.inited = false;
 }
 
@@ -443,6 +448,8 @@ int cwbl_init(const cwbl_init_params *p) {
   HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.sstream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.tstream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&S.h2d, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&S.d2h, hipStreamNonBlocking));
   {
     std::vector<double2> tab((size_t)4 * kQuadLevels * kQuadStride);  // 15, 23, 31, 63 nodes
     const int rounds[4] = {2, 3, 4, 8};
@@ -613,13 +620,22 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   const size_t bvar = (size_t)L * S.k * 4;
   hipEvent_t e2;
   HIPCHK(event(2, &e2));
-  if (sl->memory == CWBL_MEM_DEVICE) {
+  // Host-memory slab: x, y and alt go over first; var goes over batch by batch on its own
+  // stream (S.h2d) when a batch's points are contiguous in every member plane (the analysed
+  // region is the whole horizontal slab, ix_lim = nx and iy_lim = ny: point g is var word
+  // g + L m), and comes back batch by batch behind each batch's last solve (S.d2h), so the
+  // PCIe transfers overlap the kernels; otherwise (staggered U/V bounds) var moves whole.
+  const bool host = sl->memory != CWBL_MEM_DEVICE;
+  const bool piped = host && sl->ix_lim == sl->nx && sl->iy_lim == sl->ny;
+  const bool piped_back = piped && !vp->tune_q;  // tune_q touches the whole slab afterwards
+  if (!host) {
     sd.x = sl->x; sd.y = sl->y; sd.alt = sl->alt; sd.var = sl->var;
   } else {
     HIPCHK(stage(S.sx, sl->x, bxy, CWBL_MEM_HOST));
     HIPCHK(stage(S.sy, sl->y, bxy, CWBL_MEM_HOST));
     HIPCHK(stage(S.salt, sl->alt, balt, CWBL_MEM_HOST));
-    HIPCHK(stage(S.svar, sl->var, bvar, CWBL_MEM_HOST));
+    if (piped) HIPCHK(S.svar.ensure(bvar));
+    else HIPCHK(stage(S.svar, sl->var, bvar, CWBL_MEM_HOST));
     sd.x = S.sx.as<float>(); sd.y = S.sy.as<float>(); sd.alt = S.salt.as<float>();
     sd.var = S.svar.as<float>();
   }
@@ -733,10 +749,20 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     }
     HIPCHK(hipEventRecord(b, ss));
     HIPCHK(hipStreamWaitEvent(S.stream, b, 0));
+    if (piped) {  // this batch's var columns: k rows of nb floats, member pitch L
+      hipEvent_t hv;
+      HIPCHK(cevent(cev++, &hv));
+      const size_t pitch = (size_t)L * 4;
+      HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + g0, pitch, sl->var + g0, pitch,
+                              (size_t)nb * 4, (size_t)S.k, hipMemcpyHostToDevice, S.h2d));
+      HIPCHK(hipEventRecord(hv, S.h2d));
+      HIPCHK(hipStreamWaitEvent(S.stream, hv, 0));
+    }
     HIPCHK(hipEventRecord(b2, S.stream));
     if ((S.kp == 96 || S.kp == kBigSplitKP) && S.big_split && S.k > big_split_j0(S.kp) + 2) {
       // 256-thread assembly + first kBigJ0 steps -> workspace -> one-wavefront tail, in
-      // hand-off batches of Bs points (a multiple of kListLanes; ~100 KB per point)
+      // hand-off batches of Bs points (a multiple of kListLanes; BigHandoff<128, 64> is
+      // 134.7 KB per point, 4.4 GB at the default 32 768, outside workspace_bytes)
       const long long nsub = (nb + S.big_sub - 1) / S.big_sub;
       long long Bs = (nb + nsub - 1) / nsub;
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
@@ -819,6 +845,12 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       HIPCHK(hipEventRecord(cc, S.stream));
       HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), nb, dst));
     }
+    if (piped_back) {  // the batch's analysis back to the caller behind its last solve
+      HIPCHK(hipStreamWaitEvent(S.d2h, cc, 0));
+      const size_t pitch = (size_t)L * 4;
+      HIPCHK(hipMemcpy2DAsync(sl->var + g0, pitch, S.svar.as<float>() + g0, pitch,
+                              (size_t)nb * 4, (size_t)S.k, hipMemcpyDeviceToHost, S.d2h));
+    }
     search_ev.push_back({ev, ev + 1});
     solve_ev.push_back({ev + 2, ev + 3});
     done_ev.push_back(ev + 4);
@@ -835,10 +867,15 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     solve_ev.push_back({ev, ev + 1});
     ev += 2;
   }
-  hipEvent_t e_end;
+  hipEvent_t e_end, e_back;
   HIPCHK(event(ev, &e_end));
-  if (sl->memory != CWBL_MEM_DEVICE)
+  HIPCHK(event(ev + 1, &e_back));
+  if (host && !piped_back)
     HIPCHK(hipMemcpyAsync(sl->var, S.svar.p, bvar, hipMemcpyDeviceToHost, S.stream));
+  if (piped_back) {  // the call returns after the last batch's copy back
+    HIPCHK(hipEventRecord(e_back, S.d2h));
+    HIPCHK(hipStreamWaitEvent(S.stream, e_back, 0));
+  }
   HIPCHK(hipEventRecord(e_end, S.stream));
   DevStats ds;
   HIPCHK(hipMemcpyAsync(&ds, S.stats.p, sizeof ds, hipMemcpyDeviceToHost, S.stream));
@@ -863,7 +900,9 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   } else {
     for (auto &p : solve_ev) st.ms_solve += elapsed(p.first, p.second);
   }
-  st.ms_copy = elapsed(1, 2) + (sl->memory != CWBL_MEM_DEVICE ? elapsed(ev - 1, ev) : 0.0f);
+  // copies: x, y, alt (+ var when not piped) before the batches, var back after the last
+  // solve; piped transfers overlap the batches and are not counted here
+  st.ms_copy = elapsed(1, 2) + (host && !piped_back ? elapsed(ev - 1, ev) : 0.0f);
   st.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
   if (stats) *stats = st;
   return CWBL_OK;

@@ -24,6 +24,11 @@ static __constant__ unsigned long long kExpT[32] = {
 
 // exp(real(4)) as the reference build evaluates it: glibc 2.35 expf, FMA variant
 // (table-driven, computed in double; the reference's flang `exp` calls libm expf).
+// Attribution: the table kExpT and the polynomial constants below are those of glibc's
+// sysdeps/ieee754/flt-32/e_expf.c / e_exp2f_data.c (Szabolcs Nagy, ARM Ltd., 2017; GNU
+// LGPL 2.1+), reproduced so that the weight 1/(err * exp(r2/4)) rounds exactly as the
+// reference's does (module_letkf_core.f90:444; checked on all floats in [0, 8),
+// oracle/tools/expf_check.c).
 __device__ __forceinline__ float expf_ref(float x, const unsigned long long *tab = kExpT) {
   const unsigned ux = __float_as_uint(x);
   const unsigned abstop = (ux >> 20) & 0x7ffu;
@@ -401,17 +406,6 @@ __device__ __forceinline__ int stage_columns(
   return ptot;
 }
 
-// Analysis-path staging for the one-wavefront matrix-core assembly: two chunks per round
-// (stage_columns_pair) or one (stage_columns); build with -DCWBL_STAGE_PAIR=0 for the latter.
-#ifndef CWBL_STAGE_PAIR
-#define CWBL_STAGE_PAIR 1
-#endif
-constexpr bool kStagePair = CWBL_STAGE_PAIR != 0;
-#ifndef CWBL_PAIR_PIPE
-#define CWBL_PAIR_PIPE 1
-#endif
-constexpr bool kPairPipe = CWBL_PAIR_PIPE != 0;
-
 // The value of lane i ^ 32 (the other half wave), by one v_permlane32_swap.
 __device__ __forceinline__ int other_half(int x, int half) {
   const auto s = __builtin_amdgcn_permlane32_swap(x, x, false, false);
@@ -508,14 +502,11 @@ __device__ __forceinline__ int stage_columns_pair(
       }
       put(g, half ? w_x : w);
       const bool two = base + CHUNK < npairs;  // wave-uniform
-      if constexpr (kPairPipe) {  // chunk c + 1's bg rows in flight during chunk c's MFMAs
-        if (two) gather_bg(col_b, g);
-      }
+      if (two) gather_bg(col_b, g);  // chunk c + 1's bg rows in flight during chunk c's MFMAs
       __syncthreads();
       accumulate(min(CHUNK, npairs - base));
       __syncthreads();
       if (two) {
-        if constexpr (!kPairPipe) gather_bg(col_b, g);
         if (half == 1) {
           ch.yo[sl] = yo;
           if constexpr (PITCH > KP) ch.yb[sl][KP] = yo;
@@ -714,41 +705,20 @@ struct MfmaLayout {
   static constexpr bool SPLIT_LAST = NBL4 < 4;
 };
 
-// DIAG4: the diagonal 16x16 tiles of the full tile rows (I < NT-1 with SPLIT_LAST) are not
-// 16x16 products (64 matrix-pipe cycles, 120 of their 256 entries above the diagonal) but
-// three v_mfma_f64_4x4x4f64 (48 cycles) into dg[I][s]: A = tile I's operand (block b = rows
-// 16I+4b..+3), B = the same operand with its 4-lane blocks rotated by s within each 16-lane
-// row (DPP row_ror:4s), so block b of dg[I][s] is C(block b, block (b - s) mod 4) (see
-// kRorDown): s = 0 the 4 diagonal blocks, s = 1 (1,0), (2,1), (3,2) and (0,3) = (3,0)^T,
-// s = 2 (2,0), (3,1) and two duplicates.  The record kernel writes these; solve_tq_kernel
-// keeps the tiles.
-// DPP row_ror:n: lane i of a 16-lane row reads lane (i - n) mod 16.
-constexpr bool kRorDown = true;
-#ifndef CWBL_DIAG4
-#define CWBL_DIAG4 0
-#endif
-constexpr bool kDiag4 = CWBL_DIAG4 != 0;
-
-template <int KP, int CHUNK, bool ASSEMBLED, bool DIAG4 = false>
+template <int KP, int CHUNK, bool ASSEMBLED>
 __device__ __forceinline__ void assemble_point_mfma(
     ColumnChunk<KP, CHUNK, float, MfmaLayout<KP>::PITCH> &ch, const TreeDesc *__restrict__ trees,
     const SolveConsts &c, int gi, int lane, const int *__restrict__ nbr_cnt,
     const int *__restrict__ nbr_idx, const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in,
-    f64x4 (&tile)[MfmaLayout<KP>::NTL], double &b1acc, int &ptot,
-    double (*dg)[3] = nullptr) {
+    f64x4 (&tile)[MfmaLayout<KP>::NTL], double &b1acc, int &ptot) {
   using L = MfmaLayout<KP>;
-  static_assert(!DIAG4 || L::SPLIT_LAST, "DIAG4 covers the full tile rows");
-  if constexpr (DIAG4) {
-#pragma unroll
-    for (int I = 0; I + 1 < L::NT; ++I) dg[I][0] = dg[I][1] = dg[I][2] = 0.0;
-  }
 #pragma unroll
   for (int t = 0; t < L::NTL; ++t) tile[t] = f64x4{0.0, 0.0, 0.0, 0.0};
   b1acc = 0.0;
   const int kk = lane >> 4, m = lane & 15;
   auto stage = [&](auto &&acc) {
-    if constexpr (!ASSEMBLED && CHUNK == 32 && kStagePair)
+    if constexpr (!ASSEMBLED && CHUNK == 32)
       return stage_columns_pair<KP, CHUNK, MfmaLayout<KP>::PITCH>(ch, trees, c, gi, lane, nbr_cnt,
                                                                   nbr_idx, pt, acc);
     else
@@ -807,12 +777,6 @@ __device__ __forceinline__ void assemble_point_mfma(
 #pragma unroll
                 for (int r = 0; r < NS; ++r)
                   tile[t][r] = __builtin_amdgcn_mfma_f64_4x4x4f64(os[r], op[J], tile[t][r], 0, 0, 0);
-              } else if (DIAG4 && I == J) {
-                dg[I][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(op[I], op[I], dg[I][0], 0, 0, 0);
-                dg[I][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(op[I], dpp_f64<0x124>(op[I]),
-                                                              dg[I][1], 0, 0, 0);
-                dg[I][2] = __builtin_amdgcn_mfma_f64_4x4x4f64(op[I], dpp_f64<0x128>(op[I]),
-                                                              dg[I][2], 0, 0, 0);
               } else {
                 tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[I], op[J], tile[t], 0, 0, 0);
               }

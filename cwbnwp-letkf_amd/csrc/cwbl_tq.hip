@@ -640,42 +640,97 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   if (lane == 0 && info) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
 }
 
-// Stage + assemble only (the default KP = 40 split): the MFMA tiles of [Yb; yo][Yb; yo]^T go
-// straight from their C/D registers (row = 16 I + (lane >> 4) + 4 r, col = 16 J + (lane & 15))
-// to the record, packed lower, with inflat on the live diagonal and 1 on the padding's
-// (decoupled unit rows, as solve_tq_kernel's blocks); row KP of the product is b1 = Yb d.
-#ifndef CWBL_RECORD_WAVES
-#define CWBL_RECORD_WAVES 4
-#endif
-constexpr int kRecordWaves = CWBL_RECORD_WAVES;
-template <int KP, int WAVES = 5>
+// Stage + assemble only (the default KP = 40 split), one point per wavefront, into the record
+// (AsmRecord): A = inflat I + Yb Yb^T packed lower (inflat on the live diagonal, 1 on the
+// padding's: decoupled unit rows, as solve_tq_kernel's blocks) and b1 = Yb d.
+//
+// The product of the staged rows Y' = [Yb (rows 0..39); yo (row 40)] is covered with
+//   three v_mfma_f64_16x16x4 tiles  (A rows x B cols; C/D lane: col = lane & 15, row =
+//                                    (lane >> 4) + 4 reg)
+//     T0 = {yo, 1..15} x {0..15}      yo . Yb(0..15) = b1(0..15) and A(1..15, 0..15) lower
+//     T1 = {16..31}    x {0..15}      A(16..31, 0..15)
+//     T2 = {yo, 17..31} x {16..31}    b1(16..31) and A(17..31, 16..31) lower
+//   four v_mfma_f64_4x4x4_4b strips  rows 32..35 / 36..39 (broadcast over the 4 blocks) x
+//                                    tile column J's own 16x16 operand (J = 0, 1): A(32..39,
+//                                    0..31); result lane 16 i + 4 b + j = (32 + 4 r + i,
+//                                    16 J + 4 b + j)
+//   one 4x4x4_4b corner             four blocks (rows x cols) 32..35 x {yo,32,33,34},
+//                                    36..39 x {yo,35,36,37}, 36..39 x {32,33,34,38} and
+//                                    {35,39,0,16} x {35,39,0,16}: A(32..39, 32..39) lower,
+//                                    b1(32..39) and the diagonals A(0,0), A(16,16) that the
+//                                    yo rows of T0 and T2 displaced
+// = 3 x 64 + 5 x 16 = 272 matrix-pipe cycles per 4 columns for the 860 needed entries (215
+// cycles of work; 1.27x), against 336 for the 48 x 48 tiling with a yo strip (1.56x).  Every
+// entry is one fp64 FMA chain over the columns in staging order, like the reference's
+// dsyrk/dgemv (products of fp32 values are exact in fp64).
+template <int WAVES>
 __global__ void __launch_bounds__(64, WAVES)
 assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
                        long long g0, int npts, const int *__restrict__ nbr_cnt,
                        const int *__restrict__ nbr_idx, int2 *__restrict__ info,
                        double *__restrict__ ws) {
-  using L = MfmaLayout<KP>;
+  constexpr int KP = kTq4KP, PITCH = 48, YO = KP;
+  static_assert(KP == 40 && MfmaLayout<KP>::PITCH == PITCH, "the cover is laid out for KP = 40");
   using HO = AsmRecord<KP>;
-  static_assert(L::YO_ROW, "b1 rides in the padding row");
-  __shared__ ColumnChunk<KP, kTqChunk, TqStage, L::PITCH> ch;
+  __shared__ ColumnChunk<KP, kTqChunk, float, PITCH> ch;
   const int gi = xcd_remap(blockIdx.x, gridDim.x);
   if (gi >= npts) return;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x, kk = lane >> 4, m = lane & 15;
   float3 pt;
   slab_point(slab, g0 + gi, pt.x, pt.y, pt.z);
-  f64x4 tile[L::NTL];
-  double dg[L::NT][3];
-  double b1acc;
-  int ptot;
-  assemble_point_mfma<KP, kTqChunk, false, kDiag4>(ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt,
-                                                   nullptr, nullptr, nullptr, tile, b1acc, ptot,
-                                                   dg);
+  // corner operands of this lane (m = 4 b + i for the A rows, 4 b + j for the B columns)
+  auto pick = [](const int (&t)[16], int i) {
+    int v = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v = i == q ? t[q] : v;
+    return v;
+  };
+  constexpr int kRowA[16] = {32, 33, 34, 35, 36, 37, 38, 39, 36, 37, 38, 39, 35, 39, 0, 16};
+  constexpr int kColB[16] = {YO, 32, 33, 34, YO, 35, 36, 37, 32, 33, 34, 38, 35, 39, 0, 16};
+  const int ra = pick(kRowA, m), cb = pick(kColB, m);
+  f64x4 t0 = {0.0, 0.0, 0.0, 0.0}, t1 = t0, t2 = t0;
+  double st[4] = {0.0, 0.0, 0.0, 0.0}, cn = 0.0;
+  const int ptot = stage_columns_pair<KP, kTqChunk, PITCH>(
+      ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, [&](int nsl) {
+        // column s = 4 g + kk of the chunk is k-slot kk of group g; staged columns past nsl
+        // are zero.  The group loop is unrolled with a static double buffer: group g + 1's
+        // operands are read before group g's MFMAs.
+        float f[2][7];
+        auto load = [&](int b, int sc) {
+          const float *col = ch.yb[sc];
+          f[b][0] = col[m];
+          f[b][1] = col[16 + m];
+          f[b][2] = col[YO];
+          f[b][3] = col[32 + (m & 3)];
+          f[b][4] = col[36 + (m & 3)];
+          f[b][5] = col[ra];
+          f[b][6] = col[cb];
+        };
+        const int nl = c.debug_stop == 11 ? 0 : nsl;
+        if (nl > 0) load(0, kk);
+#pragma unroll
+        for (int g = 0; g < kTqChunk / 4; ++g) {
+          if (4 * g >= nl) break;  // nsl is wave-uniform
+          const int b = g & 1;
+          const double o0 = (double)f[b][0], o1 = (double)f[b][1], oy = (double)f[b][2];
+          const double a0 = m == 0 ? oy : o0, a1 = m == 0 ? oy : o1;
+          const double s0 = (double)f[b][3], s1 = (double)f[b][4];
+          const double ca = (double)f[b][5], cbv = (double)f[b][6];
+          if (g + 1 < kTqChunk / 4 && 4 * (g + 1) < nl) load(b ^ 1, 4 * (g + 1) + kk);
+          t0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, o0, t0, 0, 0, 0);
+          t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(o1, o0, t1, 0, 0, 0);
+          t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, o1, t2, 0, 0, 0);
+          st[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(s0, o0, st[0], 0, 0, 0);
+          st[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(s1, o0, st[1], 0, 0, 0);
+          st[2] = __builtin_amdgcn_mfma_f64_4x4x4f64(s0, o1, st[2], 0, 0, 0);
+          st[3] = __builtin_amdgcn_mfma_f64_4x4x4f64(s1, o1, st[3], 0, 0, 0);
+          cn = __builtin_amdgcn_mfma_f64_4x4x4f64(ca, cbv, cn, 0, 0, 0);
+        }
+      });
   if (lane == 0) info[gi] = make_int2(ptot, 0);  // p = 0: the solve leaves var unchanged
   if (ptot == 0) return;
   if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the record
-    double t = 0.0;
-#pragma unroll
-    for (int q = 0; q < L::NTL; ++q) t += tile[q][0] + tile[q][3];
+    const double t = t0[0] + t1[1] + t2[2] + st[0] + st[3] + cn;
     if (lane == 0) info[gi] = make_int2(ptot, (int)t);
     return;
   }
@@ -685,51 +740,39 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   auto put = [&](int row, int col, double a) {  // packed lower; inflat on the live diagonal
     w[HO::TA + row * (row + 1) / 2 + col] = row != col ? a : row < k ? a + inflat : 1.0;
   };
-  if constexpr (kDiag4) {
-    // dg[I][s], result lane 16i + 4b + j: C(16I + 4b + i, 16I + 4bc + j), bc = (b -/+ s) & 3
-    const int i = lane >> 4, b = (lane >> 2) & 3, j = lane & 3;
 #pragma unroll
-    for (int I = 0; I + 1 < L::NT; ++I) {
-      const int r0 = 16 * I + 4 * b + i;
-      if (i >= j) put(r0, 16 * I + 4 * b + j, dg[I][0]);
-#pragma unroll
-      for (int sh = 1; sh <= 2; ++sh) {
-        const int bc = (kRorDown ? b - sh : b + sh) & 3;
-        const double a = dg[I][sh];
-        if (bc < b) put(r0, 16 * I + 4 * bc + j, a);                           // lower block
-        else if (sh == 1) put(16 * I + 4 * bc + j, 16 * I + 4 * b + i, a);     // (b, b+-1)^T
-        // sh == 2, bc > b: the transpose of a lower block written by its other lane
-      }
+  for (int r = 0; r < 4; ++r) {
+    const int i = kk + 4 * r;  // A-operand row index of the tiles
+    if (i == 0) {
+      w[HO::U1 + m] = t0[r];        // yo . Yb(m)
+      w[HO::U1 + 16 + m] = t2[r];   // yo . Yb(16 + m)
+    } else {
+      if (m <= i) put(i, m, t0[r]);
+      if (m <= i) put(16 + i, 16 + m, t2[r]);
     }
+    put(16 + i, m, t1[r]);
   }
-  int t = 0;
 #pragma unroll
-  for (int I = 0; I < L::NT; ++I)
+  for (int r = 0; r < 2; ++r)
 #pragma unroll
-    for (int J = 0; J <= I; ++J, ++t) {
-      if (kDiag4 && I == J && I + 1 < L::NT) continue;  // written from dg above
-      const int col = 16 * J + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * I + (lane >> 4) + 4 * r;
-        if (row < KP && col <= row) {
-          const double a = tile[t][r];
-          w[HO::TA + row * (row + 1) / 2 + col] = row != col ? a : row < k ? a + inflat : 1.0;
-        } else if (row == KP && col < KP) {
-          w[HO::U1 + col] = tile[t][r];
-        }
-      }
-    }
+    for (int J = 0; J < 2; ++J) put(32 + 4 * r + kk, 16 * J + m, st[2 * J + r]);
+  {  // corner: lane 16 i + 4 b + j = (row kRowA[4 b + i], col kColB[4 b + j])
+    const int bb = (lane >> 2) & 3, i = kk, j = lane & 3;
+    const int row = pick(kRowA, 4 * bb + i), col = pick(kColB, 4 * bb + j);
+    if (col == YO) w[HO::U1 + row] = cn;
+    else if (bb == 3 ? i == j : col <= row) put(row, col, cn);
+  }
 }
+
+constexpr int kRecordWaves = 4;  // waves per SIMD of the record kernel
 
 hipError_t launch_assemble_record(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
                                   SlabDev slab, long long g0, int npts, const int *nbr_cnt,
                                   const int *nbr_idx, int2 *info, double *ws) {
   if (npts <= 0) return hipSuccess;
   if (kp != kTq4KP) return hipErrorInvalidValue;
-  // 5 waves per SIMD (96 VGPRs, 7 spilled): 0.7% faster per C2 step than 4 (110 VGPRs)
-  hipLaunchKernelGGL((assemble_record_kernel<kTq4KP, kRecordWaves>), dim3(npts), dim3(64), 0, s, trees, c,
-                     slab, g0, npts, nbr_cnt, nbr_idx, info, ws);
+  hipLaunchKernelGGL((assemble_record_kernel<kRecordWaves>), dim3(npts), dim3(64), 0, s, trees,
+                     c, slab, g0, npts, nbr_cnt, nbr_idx, info, ws);
   return hipGetLastError();
 }
 

@@ -93,7 +93,10 @@ typedef struct cwbl_init_params {
   float  norain_value;     /* control_nml norain_value (module_config.f90:295) */
   int    q1_mode;          /* CWBL_Q1_* */
   int    reserved;
-  size_t workspace_bytes;  /* device workspace budget for neighbour lists (0 = 2 GiB) */
+  size_t workspace_bytes;  /* device workspace budget for neighbour lists (0 = 2 GiB); the
+                            * solve's per-batch records come on top: 6.9 KB per point of a
+                            * search batch at k = 25..40 (two buffers), 135 KB per point of a
+                            * k = 65..128 hand-off sub-batch (CWBL_BIG_SUB, 32 768 points) */
 } cwbl_init_params;
 
 /* One GTS platform: type(gts_structure), module_gts_omboma.f90:13-22. */

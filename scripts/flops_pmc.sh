@@ -9,7 +9,7 @@ mkdir -p $OUT
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1
 grep -E "^[[:space:]]*SQ_INSTS_VALU_(FMA|ADD|MUL|TRANS)_F64|MFMA_MOPS_F64" $OUT/counters_list.txt | head -20
 P="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_WAVES"
-timeout -s KILL 240 rocprofv3 --pmc $P --kernel-include-regex "solve|assemble" -d $OUT/p1 -o p1 --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-cycle > $OUT/p1.log 2>&1 || { echo "pmc pass failed"; tail -5 $OUT/p1.log; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc $P --kernel-include-regex "solve|assemble" -d $OUT/p1 -o p1 --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-cycle --no-detail-configs > $OUT/p1.log 2>&1 || { echo "pmc pass failed"; tail -5 $OUT/p1.log; exit 1; }
 python3 - $OUT <<'PY'
 import csv, glob, sys, json, collections
 agg = collections.defaultdict(lambda: collections.defaultdict(list))

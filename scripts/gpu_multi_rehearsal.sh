@@ -3,6 +3,6 @@
 # device), then rank 0's share of the C2 grid timed alone at world 1, 2, 4, 8
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-timeout -k 10 300 env CWBL_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --no-cycle > gpurun_out/bench_n2_gloo.log 2>&1 || { echo "n2 failed"; tail -20 gpurun_out/bench_n2_gloo.log; exit 3; }
+CWBL_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 3 --warmup 1 --no-cycle --no-detail-configs > gpurun_out/bench_n2_gloo.log 2>&1 || { echo "n2 failed"; tail -20 gpurun_out/bench_n2_gloo.log; exit 3; }
 grep '^{' gpurun_out/bench_n2_gloo.log | cut -c1-700
 timeout -k 10 300 python scripts/shard_rehearsal.py 1 2 4 8 2>&1 | grep world

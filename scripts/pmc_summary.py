@@ -39,11 +39,10 @@ def main(src, tag):
             e["hbm_bytes_per_launch_corrected"] = (2 * fetch[k] + (write.get(k) or 0)) * 1024
         out["kernels"][k] = e
     names = list(out["kernels"])
-    # the solve: the split KP=40 pair (assemble_record_kernel, then solve_tq40_kernel; or the
-    # earlier assembly + 8 steps, then solve_tq4_kernel), one launch of each per batch, or the
-    # single solve kernel
+    # the solve: the split KP=40 pair (assemble_record_kernel, then solve_tq40_kernel), one
+    # launch of each per batch, or the single solve kernel
     solve = [k for k in names if "assemble_record_kernel" in k or "solve_tq40_kernel" in k] or \
-        [k for k in names if "solve_tq_kernel" in k or "solve_tq4_kernel" in k] or \
+        [k for k in names if "solve_tq_kernel" in k] or \
         [k for k in names if "solve_kernel" in k]
     solve.sort(key=lambda k: "assemble" not in k)
     short = lambda k: k.replace("void ", "").replace("cwbl::", "")  # noqa: E731

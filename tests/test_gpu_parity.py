@@ -846,3 +846,28 @@ def test_ingested_obs_set_analysis_vs_oracle():
     assert st.solved == ost.solved > 0 and st.nobs_sum == ost.nobs_sum
     rel = increment_rel_rms(var, ref, var0)
     assert rel <= INCR_TOL, rel
+
+
+@pytest.mark.parametrize("tune_q", [0, 1])
+def test_pipelined_host_slab_equals_device_slab(tune_q, monkeypatch):
+    """A host-memory slab whose analysed region is the whole horizontal slab moves var batch
+    by batch (H2D before each batch's solve on its own stream, D2H behind each batch's last
+    solve; with tune_q the copy back waits for the whole slab): bit-identical to the
+    device-memory call, over many batches."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("CWBL_MAX_BATCH", "3000")
+    _cores.clear()
+    w = _radar_case_scaled(0.1, nz=12)
+    vp = w.vp
+    vp.tune_q = tune_q
+    c = abi.Core(w.k, device=0)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    hv = w.var.copy()
+    st = c.analyze_var(vp, abi.make_slab(w.x, w.y, w.alt, hv))
+    dev = torch.device("cuda:0")
+    x, y, alt, dv = (torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                     for a in (w.x, w.y, w.alt, w.var.copy()))
+    c.analyze_var(vp, abi.make_slab(x, y, alt, dv, memory=abi.MEM_DEVICE))
+    c.finalize()
+    assert st.solved > 0
+    np.testing.assert_array_equal(hv.view(np.uint32), dv.cpu().numpy().view(np.uint32))
