@@ -20,11 +20,11 @@
 //     sum_c A(c, i) v_c over the slot rows (one 16-lane reduction per prefix row);
 //   - the update of the slots covers columns j+1 .. KP-1, which includes the prefix rows'
 //     entries right of the block; the block itself is updated on lanes < J0.
-// After J0 steps the trailing (KP-J0)^2 matrix sits in exactly the layout of
-// solve_tq4_kernel's steps (phase 2), and every reflector stays in the registers of the
-// column it eliminated (slot columns j, prefix register j), so nothing of the
-// tridiagonalisation goes through memory.  Every loop over steps, slots and columns is
-// compile-time (sfor), so all register indices are static.
+// After J0 steps the trailing (KP-J0)^2 matrix is held as 16-lane rows (phase 2).  Phase 1's
+// reflectors go to LDS as they are formed; phase 2's stay in the registers of the column
+// they eliminated.  Nothing is written to global memory but the analysis, and the kernel
+// spills no registers (243 VGPRs, two waves per SIMD, 19.4 KB of LDS per wave).  Every loop
+// over steps, slots and columns is compile-time (sfor), so all register indices are static.
 #include "cwbl_device.h"
 
 #include <utility>
@@ -62,9 +62,10 @@ __device__ __forceinline__ double ror8(double x) { return dpp_f64<0x128>(x); }
 
 template <int KP>
 struct Tq40Smem {
-  static constexpr int QLD = 9;  // 8 nodes per quadrature round (+1 against bank conflicts)
-  double qx[4][KP][QLD];         // per round: omega_n x_n(row) of the 8 nodes
-  double tq[4][KP + 1][4];       // d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
+  double pv[4][kTq40J0][KP];  // phase 1's reflectors, column j by row (rows <= j + 1 unused)
+  double qs[4][KP];           // per quadrature round: sum over the round's nodes of omega x(row)
+  double qz[4][KP + 1];       // T^-1 u2 (slot 7 of the last round); [KP]: other lanes' dump
+  double tq[4][KP + 1][4];    // d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
   double tau[4][KP];
 };
 
@@ -91,16 +92,10 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   const int k = c.k;
   const int ptot = valid ? info[gi].x : 0;
   // record words of this point: SGPR base + 32-bit offset (the host keeps a batch's records
-  // below 2^32 bytes).  A lane past the batch works on the spare record npts (the host
-  // allocates npts + 1): it parks into it, so it must not share a live point's record
+  // below 2^32 bytes).  A lane past the batch reads the spare record npts (the host
+  // allocates npts + 1)
   const unsigned wb = (unsigned)(valid ? gi : npts) * (unsigned)HO::WORDS;
   auto w = [&](int i) { return gld(ws, wb + (unsigned)i); };
-  // phase 1's reflectors are parked in the record's consumed A words between the end of
-  // phase 1 and the back-transform: column j of vector slot vs at word park(j, vs) + l
-  auto park = [](int j, int vs) { return 16 * (NV * j + vs); };
-  auto wst = [&](unsigned base, int i, double v) {
-    *reinterpret_cast<double *>(reinterpret_cast<char *>(ws) + (base + (unsigned)i) * 8u) = v;
-  };
   auto apk = [](int r, int col) {  // packed lower index of A(r, col)
     return col <= r ? r * (r + 1) / 2 + col : col * (col + 1) / 2 + r;
   };
@@ -170,7 +165,6 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     ub[r] = w(HO::U1 + t);
     ux[r] = t < k ? (double)xbl[r + 1] - xb_mean : 0.0;
   });
-  double trace = 0.0;  // sum of d_j, j < k
 
   // dlarfg with fp64 rcp/rsq refined to ~1 ulp; H = I when x = 0 (tau = 0, v = e_j+1)
   struct Refl {
@@ -193,7 +187,6 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   sfor<J0>([&](auto jj) {
     constexpr int j = decltype(jj)::value, J1 = j + 1;
     const double dj = rbcast<j>(Pb[j]);  // A(j,j): final diagonal of T
-    trace += j < k ? dj : 0.0;
     // alpha = A(j+1, j): prefix row j+1, or slot 0 lane 0 (row J0) at the last step
     double alpha, u2a, u1a;
     if constexpr (J1 < J0) {
@@ -229,14 +222,16 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     // v: 1 at row j + 1, x * scal below; the reflector stays in column j's registers
     const double xsP = xP * h.scal;
     double vP = (pre && l == J1) ? 1.0 : xsP;
-    Pb[j] = xsP;
     double v[NS];
+    // the reflector is final: it goes to LDS until the back-transform, and column j's
+    // registers are dead from here on
+    sm.pv[q][j][pre ? l : 0] = xsP;  // lanes >= J0: 0 into row 0, which no reflector uses
     sfor<NS>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
       const double xs = x[r] * h.scal;
       if constexpr (J1 == J0 && r == 0) v[r] = l == 0 ? 1.0 : xs;
       else v[r] = xs;
-      A[r][j] = xs;
+      sm.pv[q][j][J0 + l + 16 * r] = xs;
     });
     const double s2 = fma(h.scal, xu, u2a);  // v . x'
     const double s3 = fma(h.scal, xb, u1a);  // v . b1
@@ -307,14 +302,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       if constexpr (col < J0) Pb[col] = fma(-vP, wc, fma(-wP, vc, Pb[col]));
     });
   });
-  // park phase 1's reflectors (registers free for phase 2 and the quadrature)
-  sfor<J0>([&](auto jj) {
-    constexpr int j = decltype(jj)::value;
-    wst(wb, park(j, 0) + l, Pb[j]);
-    sfor<NS>([&](auto rr) { wst(wb, park(j, decltype(rr)::value + 1) + l, A[decltype(rr)::value][j]); });
-  });
-  // A (one-wave) workgroup barrier ends the scheduling region: without it the compiler
-  // schedules the whole straight-line phase 1 + phase 2 as one region and spills 2x as much
+  // a (one-wave) workgroup barrier: a fence the scheduler does not move phase 2 across
   __syncthreads();
   // the prefix rows of Q^T b1, Q^T x' are final (later reflectors vanish there)
   if (pre) {
@@ -323,7 +311,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   }
 
   if constexpr (STOP == 4) {  // timing ablation: phase 1 only
-    if (valid && l == 0) info[gi] = make_int2(ptot, (int)(trace + uxP + A[1][KP - 1]));
+    if (valid && l == 0) info[gi] = make_int2(ptot, (int)(uxP + A[1][KP - 1]));
     return;
   }
   // ---- phase 2: steps J0 .. KP-3 on the trailing rows (solve_tq4_kernel's step) -----------
@@ -334,7 +322,6 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     constexpr int jl = decltype(jj)::value, j = J0 + jl;
     constexpr int RJ = jl / 16, LJ = jl % 16;
     const double dj = rbcast<LJ>(A[RJ][j]);  // A(j,j): final diagonal of T
-    trace += j < k ? dj : 0.0;
     if constexpr (jl + 2 < KT) {
       constexpr int J1 = jl + 1, R1 = J1 / 16, L1 = J1 % 16;
       const double alpha = rbcast<L1>(A[R1][j]);
@@ -432,6 +419,18 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     sm.tq[q][KP][1] = 0.0;
   }
   __syncthreads();
+  // trace of T (= trace of A) over the members, from the diagonal in LDS: summed here, not
+  // step by step, so that no step's d_j stays live to the end
+  double trace;
+  {
+    double tp = 0.0;
+    sfor<(KP + 15) / 16>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      const int i = l + 16 * r;
+      if (16 * r + 15 < KP || i < KP) tp += i < k ? sm.tq[q][i < KP ? i : 0][0] : 0.0;
+    });
+    trace = row16_sum(tp);
+  }
 
   if constexpr (STOP == 2) {  // timing ablation: tridiagonalisation only
     if (valid && l == 0) info[gi] = make_int2(ptot, (int)(trace + ux[1]));
@@ -441,7 +440,9 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   // lambda^-1/2 = (2/pi) int_0^inf dt / (t^2 + lambda) with the elliptic substitution and
   // the midpoint rule on the spectrum bound [m, M] (solve_tq_kernel, cwbl_tq.hip): each node
   // is one shifted SPD tridiagonal solve, twisted: lane l & 7 is the node of the round,
-  // side l >> 3 walks rows 0..H-1 (top) or KP-1..H (bottom); node 31 solves T^-1 u2.
+  // side l >> 3 walks rows 0..H-1 (top) or KP-1..H (bottom); slot 7 of the last round solves
+  // T^-1 u2.  Each row's sum over the round's 8 nodes is an 8-lane DPP reduction; its lane 0
+  // hands it to the row's owner through LDS.
   const double m = (double)c.inflat;
   const double ratio = trace / m - (double)(k - 1);
   int level = 1;
@@ -458,9 +459,20 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   const double2 *qtab = quad_rule(c.quad_r, R, level);
   const int side = l >> 3, n8 = l & 7;
   const double(*T)[4] = sm.tq[q];
-  const double *tq0 = &T[side ? KP - 1 : 0][0];
-  const int dir = side ? -4 : 4;
-  const int cs = side ? 5 : 1;  // coupling with the previous row of the walk
+  // LDS byte offsets, walked one row per step through a register the compiler cannot see
+  // through (asm): computed addresses of every row would be loop-invariant, and hoisting
+  // them out of the round loop holds ~40 VGPRs
+  char *const smb = reinterpret_cast<char *>(&sm);
+  auto lds = [&](unsigned off) { return *reinterpret_cast<const double *>(smb + off); };
+  auto sts = [&](unsigned off, double v) { *reinterpret_cast<double *>(smb + off) = v; };
+  const unsigned tq0 = (unsigned)(offsetof(SM, tq) + (size_t)q * sizeof(sm.tq[0])) +
+                       (side ? (KP - 1) * 32u : 0u);   // row 0 of the walk
+  const unsigned dirb = side ? (unsigned)-32 : 32u;   // next row of the walk
+  const unsigned csb = side ? 40u : 8u;  // coupling with the previous row of the walk
+  const unsigned qs0 = (unsigned)(offsetof(SM, qs) + (size_t)q * sizeof(sm.qs[0])) +
+                       (side ? (KP - H) * 8u : (H - 1) * 8u);  // row H-1 of the walk
+  const unsigned qz0 = (unsigned)(offsetof(SM, qz) + (size_t)q * sizeof(sm.qz[0]));
+  const unsigned bdir = side ? 8u : (unsigned)-8;    // back-substitution: previous row
   double ys[NV], z[NV];
   sfor<NV>([&](auto vv) { ys[decltype(vv)::value] = 0.0; });
   for (int round = 0; round < R; ++round) {
@@ -469,42 +481,57 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     const double sigma = node < NQ ? m * tw.x : 0.0;
     const double omega = node < NQ ? sqrt(m) * tw.y : 1.0;
     double hh[H], mm[H];
-    double dl = tq0[0] + sigma, gt = tq0[3];
+    unsigned pw = tq0;
+    double dl = lds(pw) + sigma, gt = lds(pw + 24);
     double rdl = rcp64(dl);
     sfor<H - 1>([&](auto tt) {
       constexpr int t = decltype(tt)::value + 1;
-      const double *qt = tq0 + dir * t;
-      const double ct = qt[cs];
+      pw += dirb;
+      asm volatile("" : "+v"(pw) : "v"(dl));  // row t is read once d_{t-1} is known
+      const double ct = lds(pw + csb);
       const double lt = ct * rdl;
       hh[t - 1] = gt * rdl;
       mm[t - 1] = lt;
-      dl = fma(-lt, ct, qt[0] + sigma);
-      gt = fma(-lt, gt, qt[3]);
+      dl = fma(-lt, ct, lds(pw) + sigma);
+      gt = fma(-lt, gt, lds(pw + 24));
       rdl = rcp64(dl);
     });
     // rows H-1 (top) and H (bottom): 2x2 solve with the partner lane's pivot
     const double cm = T[H][1];
     const double dlo = ror8(dl), go = ror8(gt);
     double xv = (gt * dlo - cm * go) / fma(dl, dlo, -cm * cm);
-    auto row_of = [&](int t) { return side ? KP - 1 - t : t; };
-    sm.qx[q][row_of(H - 1)][n8] = omega * xv;
+    const bool last = round == R - 1;
+    const bool zlane = last && n8 == 7;  // T^-1 u2: not a node of the sum
+    const double om = zlane ? 0.0 : omega;
+    unsigned ps = qs0;                          // qs of the walk's current row
+    unsigned pz = qz0 + (zlane ? qs0 - (unsigned)offsetof(SM, qs) - (unsigned)q * KP * 8u
+                               : KP * 8u);     // qz of that row, or the dump word
+    const unsigned zdir = zlane ? bdir : 0u;
+    auto emit = [&](double x) {
+      double s = om * x;
+      s += dpp_f64<0xB1>(s);   // quad_perm [1,0,3,2]
+      s += dpp_f64<0x4E>(s);   // quad_perm [2,3,0,1]
+      s += dpp_f64<0x141>(s);  // row_half_mirror: the 8 lanes of the side
+      // stores without branches: the side's 8 lanes store the same sum
+      sts(ps, s);
+      sts(pz, x);
+    };
+    emit(xv);
     sfor<H - 1>([&](auto tt) {
       constexpr int t = H - 2 - decltype(tt)::value;
       xv = fma(-mm[t], xv, hh[t]);
-      sm.qx[q][row_of(t)][n8] = omega * xv;
+      ps += bdir;
+      pz += zdir;
+      asm volatile("" : "+v"(ps), "+v"(pz) : "v"(xv));
+      emit(xv);
     });
     __syncthreads();
-    const bool last = round == R - 1;  // slot 7 of the last round is T^-1 u2
     sfor<NV>([&](auto vv) {
       constexpr int vs = decltype(vv)::value;
       const int i = vrow(vs);
-      const double *row = sm.qx[q][i < KP ? i : 0];
-      double s = 0.0;
-      sfor<7>([&](auto nn) { s += row[decltype(nn)::value]; });
-      const double r7 = row[7];
-      s = last ? s : s + r7;
-      ys[vs] += i < KP ? s : 0.0;
-      if (last) z[vs] = i < KP ? r7 : 0.0;
+      const int ic = i < KP ? i : 0;
+      ys[vs] += i < KP ? sm.qs[q][ic] : 0.0;
+      if (last) z[vs] = i < KP ? sm.qz[q][ic] : 0.0;
     });
     __syncthreads();
   }
@@ -522,17 +549,6 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   }
 
   // ---- back-transform: y <- Q y = H_0 H_1 ... H_{KP-3} y ----------------------------------
-  double pv[J0][NV];  // phase 1's reflectors, loaded behind phase 2's
-  {
-    unsigned pbase = wb;
-    asm volatile("" : "+v"(pbase));  // opaque: the compiler must load, not forward the stores
-    sfor<J0>([&](auto jj) {
-      sfor<NV>([&](auto vv) {
-        constexpr int j = decltype(jj)::value, vs = decltype(vv)::value;
-        pv[j][vs] = gld(ws, pbase + (unsigned)(park(j, vs) + l));
-      });
-    });
-  }
   double y[NV];
   sfor<NV>([&](auto vv) { y[decltype(vv)::value] = ys[decltype(vv)::value]; });
   sfor<KT - 2>([&](auto jj) {  // phase 2's reflectors (rows > J0 only)
@@ -558,13 +574,15 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   sfor<J0>([&](auto jj) {  // phase 1's reflectors: prefix register j and slot column j
     constexpr int j = J0 - 1 - decltype(jj)::value, J1 = j + 1;
     const double tj = sm.tau[q][j];
-    const double v0 = !pre ? 0.0 : l == J1 ? 1.0 : pv[j][0];  // 0 at rows <= j + 1
+    const double *pj = sm.pv[q][j];
+    const double v0 = l == J1 ? 1.0 : (pre && l > J1) ? pj[lp] : 0.0;  // 0 at rows <= j + 1
     double vv[NS];
     double a = v0 * y[0];
     sfor<NS>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
-      if constexpr (J1 == J0 && r == 0) vv[r] = l == 0 ? 1.0 : pv[j][r + 1];
-      else vv[r] = pv[j][r + 1];
+      const double pr = pj[J0 + l + 16 * r];
+      if constexpr (J1 == J0 && r == 0) vv[r] = l == 0 ? 1.0 : pr;
+      else vv[r] = pr;
       a = fma(vv[r], y[r + 1], a);
     });
     a = row16_sum(a);
