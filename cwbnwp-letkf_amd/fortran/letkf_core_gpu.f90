@@ -68,10 +68,20 @@ module letkf_core_gpu
         real(c_double)       :: ms_total, ms_prep, ms_search, ms_solve, ms_copy
     end type cwbl_stats
 
+    ! projection_nml (module_config.f90:70-75), include/cwb_letkf_ingest.h
+    type, bind(C), public :: cwbl_projection
+        real(c_float) :: sta_lon, cen_lat, truelat1, truelat2
+    end type cwbl_projection
+
     public :: cwbl_init, cwbl_set_obs, cwbl_analyze_var, cwbl_solve_batch, cwbl_search, &
               cwbl_pack_columns, cwbl_unpack_columns, cwbl_vcoord_mean, &
-              cwbl_member_sum, cwbl_scale, &
+              cwbl_member_sum, cwbl_scale, cwbl_set_stream, &
               cwbl_finalize, cwbl_abi_version, cwbl_error, cwbl_check
+    ! host obs ingest (include/cwb_letkf_ingest.h); file names and varname are passed as
+    ! trim(name)//c_null_char
+    public :: cwbl_lonlat_to_xy, cwbl_ingest_create, cwbl_ingest_destroy, cwbl_ingest_read_gts, &
+              cwbl_ingest_read_radar, cwbl_ingest_obs_set, cwbl_ingest_type_meta, &
+              cwbl_ingest_wire_words, cwbl_ingest_pack_wire
 
     interface
         integer(c_int) function cwbl_init(p) bind(C, name='cwbl_init')
@@ -146,6 +156,84 @@ module letkf_core_gpu
             integer(c_long_long), value :: n
             real(c_float),        value :: alpha
         end function cwbl_scale
+
+        ! HIP stream (hipStream_t, c_null_ptr = the null stream) whose queued work device
+        ! pointers handed to the library may still depend on
+        integer(c_int) function cwbl_set_stream(stream) bind(C, name='cwbl_set_stream')
+            import :: c_int, c_ptr
+            type(c_ptr), value :: stream
+        end function cwbl_set_stream
+
+        ! proj_type%init + %lonlat_to_xy (module_projection.f90:21-50) for n points
+        integer(c_int) function cwbl_lonlat_to_xy(proj, n, lon, lat, x, y) &
+                bind(C, name='cwbl_lonlat_to_xy')
+            import :: c_int, c_long_long, c_float, cwbl_projection
+            type(cwbl_projection), intent(in)  :: proj
+            integer(c_long_long),  value       :: n
+            real(c_float),         intent(in)  :: lon(*), lat(*)
+            real(c_float),         intent(out) :: x(*), y(*)
+        end function cwbl_lonlat_to_xy
+
+        type(c_ptr) function cwbl_ingest_create(nmember, proj) bind(C, name='cwbl_ingest_create')
+            import :: c_ptr, c_int, cwbl_projection
+            integer(c_int), value             :: nmember
+            type(cwbl_projection), intent(in) :: proj
+        end function cwbl_ingest_create
+
+        subroutine cwbl_ingest_destroy(h) bind(C, name='cwbl_ingest_destroy')
+            import :: c_ptr
+            type(c_ptr), value :: h
+        end subroutine cwbl_ingest_destroy
+
+        ! read_gts_omboma (module_gts_omboma.f90:48-506) of one member; member -1: from the name
+        integer(c_int) function cwbl_ingest_read_gts(h, member, gts_file, obs_gts_file) &
+                bind(C, name='cwbl_ingest_read_gts')
+            import :: c_int, c_ptr, c_char
+            type(c_ptr),    value :: h
+            integer(c_int), value :: member
+            character(kind=c_char), intent(in) :: gts_file(*), obs_gts_file(*)
+        end function cwbl_ingest_read_gts
+
+        ! read_radar (module_radar.f90:30-118); varname 'MR', 'VR', 'MD' or 'MK'
+        integer(c_int) function cwbl_ingest_read_radar(h, member, file, varname) &
+                bind(C, name='cwbl_ingest_read_radar')
+            import :: c_int, c_ptr, c_char
+            type(c_ptr),    value :: h
+            integer(c_int), value :: member
+            character(kind=c_char), intent(in) :: file(*), varname(*)
+        end function cwbl_ingest_read_radar
+
+        ! the set read so far as a host-memory cwbl_obs_set (views into the handle)
+        integer(c_int) function cwbl_ingest_obs_set(h, os) bind(C, name='cwbl_ingest_obs_set')
+            import :: c_int, c_ptr, cwbl_obs_set
+            type(c_ptr), value                :: h
+            type(cwbl_obs_set), intent(out)   :: os
+        end function cwbl_ingest_obs_set
+
+        integer(c_int) function cwbl_ingest_type_meta(h, family, type_id, nvar, nobs, ids, lat, &
+                lon, alt) bind(C, name='cwbl_ingest_type_meta')
+            import :: c_int, c_ptr
+            type(c_ptr),    value         :: h
+            integer(c_int), value         :: family, type_id
+            integer(c_int), intent(out)   :: nvar, nobs
+            type(c_ptr),    intent(out)   :: ids, lat, lon, alt
+        end function cwbl_ingest_type_meta
+
+        ! the one-buffer wire format replacing gts_distribute / radar_distribute
+        ! (module_gts_omboma.f90:508-611, module_radar.f90:120-186): one MPI_Bcast of
+        ! cwbl_ingest_wire_words(h) reals from the reading rank
+        integer(c_long_long) function cwbl_ingest_wire_words(h) bind(C, name='cwbl_ingest_wire_words')
+            import :: c_long_long, c_ptr
+            type(c_ptr), value :: h
+        end function cwbl_ingest_wire_words
+
+        integer(c_int) function cwbl_ingest_pack_wire(h, buf, cap_words) &
+                bind(C, name='cwbl_ingest_pack_wire')
+            import :: c_int, c_long_long, c_float, c_ptr
+            type(c_ptr),          value       :: h
+            real(c_float),        intent(out) :: buf(*)
+            integer(c_long_long), value       :: cap_words
+        end function cwbl_ingest_pack_wire
 
         integer(c_int) function cwbl_finalize() bind(C, name='cwbl_finalize')
             import :: c_int

@@ -75,3 +75,24 @@ def test_fortran_host_analysis_matches_reference(name):
         assert "fortran host: solved=" in r.stdout
         var = np.fromfile(fout, np.float32).reshape(case.var_in.shape)
     assert increment_rel_rms(var, case.var_out, case.var_in) <= 1e-6
+
+
+@needs_fc
+def test_fortran_host_ingest_equals_the_python_binding(tmp_path):
+    """A Fortran host reads the member obs files through the ingest interfaces of
+    letkf_core_gpu.f90 (fortran/ingest_driver.f90) and packs the wire buffer that replaces
+    gts_distribute / radar_distribute: the same bits as the ctypes binding's."""
+    from cwbl import ingest
+    drv = os.path.join(PKG, "lib", "ingest_driver")
+    subprocess.run(["make", "-C", PKG, "fortran"], check=True, capture_output=True)
+    d = os.path.join(REPO, "tests", "golden", "ingest")
+    out = str(tmp_path / "wire.bin")
+    r = subprocess.run([drv, d, "3", out], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "gts types=8 radar types=2" in r.stdout
+    h = ingest.Ingest(3)
+    for m in range(3):
+        h.read_gts(os.path.join(d, f"gts_letkf_{m + 1:03d}"), os.path.join(d, "obs_gts"))
+        h.read_radar(os.path.join(d, f"VR_letkf_{m + 1:03d}"), "VR")
+        h.read_radar(os.path.join(d, f"MR_letkf_{m + 1:03d}"), "MR")
+    np.testing.assert_array_equal(np.fromfile(out, np.uint32), h.wire().view(np.uint32))
