@@ -125,6 +125,19 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
 }
 
 // Sum over each 16-lane row; every lane of a row gets the same (bitwise) row sum.
+// v through a register the compiler cannot see through, after `dep` is known.  The per-row
+// LDS offsets of a quadrature walk whose direction differs per lane (base + dir * t) are
+// loop-invariant: without this the compiler hoists all of them out of the pass loop and holds
+// one VGPR per row; formed from an opaque base they are computed where they are used.
+__device__ __forceinline__ unsigned opaque_after(unsigned v, double dep) {
+  asm volatile("" : "+v"(v) : "v"(dep));
+  return v;
+}
+// the double at byte offset `off` of a shared-memory object
+__device__ __forceinline__ double lds_at(const void *base, unsigned off) {
+  return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(base) + off);
+}
+
 __device__ __forceinline__ double row16_sum(double v) {
   v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]

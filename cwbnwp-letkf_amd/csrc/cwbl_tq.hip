@@ -520,9 +520,10 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   // lane side 0 walks rows 0, 1, .. H-1; side 1 walks rows KP-1, KP-2, .. H (mirrored).
   // Forward elimination towards the middle keeps, per row, h_t = g_t / dl_t and
   // m_t = c_{t+1} / dl_t, so that back substitution is x_t = h_t - m_t x_{t+1}.
-  const int dir = side ? -4 : 4;
-  const double *q = &sm.tq[side ? KP - 1 : 0][0];
-  const int cs = side ? 5 : 1;  // coupling with the previous mirrored row: c(i-1,i) / c(i,i+1)
+  // byte offsets into sm.tq: row t of the walk at q0 + dirb t (opaque_after, cwbl_device.h)
+  const unsigned q0 = side ? (KP - 1) * 32u : 0u, dirb = side ? (unsigned)-32 : 32u;
+  // coupling with the previous mirrored row: c(i-1,i) / c(i,i+1)
+  const unsigned csb = side ? 40u : 8u;
   double *ym = Ym + side * H, *zm = Zm + side * H;
   for (int pass = 0; pass < npass; ++pass) {
     const bool exact = pass == 0 && node == 31;
@@ -533,19 +534,19 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
       omega = sqrt(m) * tw.y;
     }
     double hh[H], mm[H];
-    double dl = q[0] + sigma;
-    double gt = q[3];
+    double dl = lds_at(sm.tq, q0) + sigma;
+    double gt = lds_at(sm.tq, q0 + 24);
     double rdl = rcp64(dl);
 #pragma unroll
     for (int t = 1; t < H; ++t) {
-      const double *qt = q + dir * t;
-      const double ct = qt[cs];
+      const unsigned o = opaque_after(q0, dl) + dirb * (unsigned)t;
+      const double ct = lds_at(sm.tq, o + csb);
       const double l = ct * rdl;
       hh[t - 1] = gt * rdl;
       mm[t - 1] = l;  // = c_t / dl_{t-1}
       asm volatile("" : "+v"(hh[t - 1]));  // materialise now: g_{t-1} and 1/dl_{t-1} die here
-      dl = fma(-l, ct, qt[0] + sigma);
-      gt = fma(-l, gt, qt[3]);
+      dl = fma(-l, ct, lds_at(sm.tq, o) + sigma);
+      gt = fma(-l, gt, lds_at(sm.tq, o + 24));
       rdl = rcp64(dl);
       __builtin_amdgcn_sched_barrier(0);  // keep the recurrence in order: bounded live ranges
     }

@@ -586,20 +586,20 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
       sigma = m * tw.x;
       omega = sqrt(m) * tw.y;
     }
-    const int dir = side ? -4 : 4;
-    const double *q = &sm.tq[side ? KP - 1 : 0][0];
-    const int cs = side ? 5 : 1;  // coupling with the previous mirrored row
-    // one row of the forward elimination (identical in both passes)
+    // byte offsets into sm.tq: row t of the walk at q0 + dirb t (opaque_after, cwbl_device.h)
+    const unsigned q0 = side ? (KP - 1) * 32u : 0u, dirb = side ? (unsigned)-32 : 32u;
+    const unsigned csb = side ? 40u : 8u;  // coupling with the previous mirrored row
+    // one row of the forward elimination (identical in both sweeps)
     auto fwd = [&](int t, double &dl, double &gt) {
-      const double *qt = q + dir * t;
-      const double ct = qt[cs];
+      const unsigned o = opaque_after(q0, dl) + dirb * (unsigned)t;
+      const double ct = lds_at(sm.tq, o + csb);
       const double l = ct * rcp64(dl);
-      dl = fma(-l, ct, qt[0] + sigma);
-      gt = fma(-l, gt, qt[3]);
+      dl = fma(-l, ct, lds_at(sm.tq, o) + sigma);
+      gt = fma(-l, gt, lds_at(sm.tq, o + 24));
     };
     constexpr int S = 8, NS = H / S;
     double ckd[NS], ckg[NS];
-    double dl = q[0] + sigma, gt = q[3];
+    double dl = lds_at(sm.tq, q0) + sigma, gt = lds_at(sm.tq, q0 + 24);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       ckd[s] = dl;
@@ -622,7 +622,9 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
         if (i > 0) fwd(t, d2, g2);
         const double rd = rcp64(d2);
         hh[i] = g2 * rd;
-        mmv[i] = (t + 1 < H) ? q[dir * (t + 1) + cs] * rd : 0.0;  // c_{t+1} / dl_t
+        mmv[i] = (t + 1 < H)  // c_{t+1} / dl_t
+                     ? lds_at(sm.tq, opaque_after(q0, d2) + dirb * (unsigned)(t + 1) + csb) * rd
+                     : 0.0;
       }
 #pragma unroll
       for (int i = S - 1; i >= 0; --i) {

@@ -264,19 +264,19 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       sigma = m * tw.x;
       omega = sqrt(m) * tw.y;
     }
-    const int dir = side ? -4 : 4;
-    const double *q = &sm.tq[side ? KP - 1 : 0][0];
-    const int cs = side ? 5 : 1;  // coupling with the previous row of the walk
+    // byte offsets into sm.tq: row t of the walk at q0 + dirb t (opaque_after, cwbl_device.h)
+    const unsigned q0 = side ? (KP - 1) * 32u : 0u, dirb = side ? (unsigned)-32 : 32u;
+    const unsigned csb = side ? 40u : 8u;  // coupling with the previous row of the walk
     auto fwd = [&](int t, double &dl, double &gt) {
-      const double *qt = q + dir * t;
-      const double ct = qt[cs];
+      const unsigned o = opaque_after(q0, dl) + dirb * (unsigned)t;
+      const double ct = lds_at(sm.tq, o + csb);
       const double lt = ct * rcp64(dl);
-      dl = fma(-lt, ct, qt[0] + sigma);
-      gt = fma(-lt, gt, qt[3]);
+      dl = fma(-lt, ct, lds_at(sm.tq, o) + sigma);
+      gt = fma(-lt, gt, lds_at(sm.tq, o + 24));
     };
     constexpr int S = 8, NS = H / S;
     double ckd[NS], ckg[NS];
-    double dl = q[0] + sigma, gt = q[3];
+    double dl = lds_at(sm.tq, q0) + sigma, gt = lds_at(sm.tq, q0 + 24);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       ckd[s] = dl;
@@ -298,7 +298,9 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         if (i > 0) fwd(t, d2, g2);
         const double rd = rcp64(d2);
         hh[i] = g2 * rd;
-        mmv[i] = (t + 1 < H) ? q[dir * (t + 1) + cs] * rd : 0.0;  // c_{t+1} / dl_t
+        mmv[i] = (t + 1 < H)  // c_{t+1} / dl_t
+                     ? lds_at(sm.tq, opaque_after(q0, d2) + dirb * (unsigned)(t + 1) + csb) * rd
+                     : 0.0;
       }
 #pragma unroll
       for (int i = S - 1; i >= 0; --i) {

@@ -51,9 +51,10 @@ def test_pack_unpack_vs_oracle(nz, ny, nx, world):
 @pytest.mark.parametrize("side_stream", [False, True])
 def test_device_inputs_only_need_to_be_queued(side_stream):
     """The library's streams are non-blocking; every device-pointer entry point must wait for
-    work the caller has merely queued (a NaN fill queued on torch's stream landed
-    after unpack_columns had written its output).  The producer here is held back by a GPU
-    spin, on torch's current stream or on a side stream, and the library is called at once."""
+    work the caller has merely queued on its stream (a NaN fill queued on torch's
+    stream landed after unpack_columns had written its output).  The producer here is held
+    back by a GPU spin, on torch's current stream or on a side stream named by
+    cwbl_set_stream, and the library is called at once."""
     c = core()
     nz, ny, nx, world = 4, 33, 65, 12
     px, py = tr.dims_create(world)
@@ -62,6 +63,7 @@ def test_device_inputs_only_need_to_be_queued(side_stream):
     send = torch.zeros((nz * ny * nx,), device="cuda")
     torch.cuda.synchronize()
     s = torch.cuda.Stream() if side_stream else torch.cuda.current_stream()
+    c.set_stream(s)
     with torch.cuda.stream(s):
         torch.cuda._sleep(20_000_000)  # ~10 ms of GPU spin before the input is written
         f.copy_(g)
@@ -73,6 +75,7 @@ def test_device_inputs_only_need_to_be_queued(side_stream):
         back.fill_(float("nan"))
     c.unpack_columns(send, nx, ny, nz, px, py, back)
     torch.cuda.synchronize()
+    c.set_stream(None)
     assert torch.equal(back, g)
 
 
