@@ -122,13 +122,17 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   });
   // fp32 sum over members in member order; member m is row m: prefix slot lane m (m < J0),
   // else row slot (m - J0) / 16, lane (m - J0) % 16
+  // (the member masks m < k are recomputed per call from an opaque copy of k: kept from the
+  // prologue to the epilogue they are 40 SGPR pairs, spilled to VGPR lanes)
   auto seq_sum_f32 = [&](const float (&x)[NV]) {
+    int kk = k;
+    asm volatile("" : "+s"(kk));
     float s = 0.0f;
     sfor<KP>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
       constexpr int vs = m < J0 ? 0 : 1 + (m - J0) / 16, ln = m < J0 ? m : (m - J0) % 16;
       const float b = rbcast<ln>(x[vs]);
-      s = s + (m < k ? b : 0.0f);  // s + 0 = s: s is never -0
+      s = s + (m < kk ? b : 0.0f);  // s + 0 = s: s is never -0
     });
     return s;
   };
