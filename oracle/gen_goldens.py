@@ -287,6 +287,65 @@ def main_dims():
         json.dump(manifest, f, indent=1, sort_keys=True)
 
 
+def driver_cases():
+    gts5 = dict(err_muti=[0.5] * 5, err_rej=[5.0] * 5)
+    return [
+        # C1: 10x10x5, k=8, 50 synop obs at the surface (BASELINE.json configs[0])
+        ("driver_c1.npz", 401, dict(k=8, nx=10, ny=10, nz=5, ix_lim=10, iy_lim=10,
+          types=[T(0, 2, 50, 50.0, 3.0, 100, upper=False, **gts5)], ztop=6e3)),
+        # mixed GTS + radar, truncation (max_lz small), QC/gross/norain rejects, Q2 bounds
+        ("driver_mixed.npz", 402, dict(k=16, nx=12, ny=9, nz=6, ix_lim=11, iy_lim=9,
+          types=[T(0, 1, 30, 75.0, 3.0, 12, err_muti=[0.5, 0.5, 0.7, 0.5, 0.5]),
+                 T(0, 2, 40, 50.0, 3.0, 100, upper=False, is_assim=[1, 1, 0, 1, 1], **gts5),
+                 T(0, 10, 25, 50.0, 3.0, 9, **gts5),
+                 T(1, 1, 400, 8.0, 2.0, 30, err_muti=2.5, err_rej=20.0),
+                 T(1, 2, 500, 12.0, 3.0, 300, err_muti=1.0, err_rej=8.0)])),
+        # Gaspari-Cohn weighting, k = 40
+        ("driver_gc_k40.npz", 403, dict(k=40, nx=8, ny=7, nz=5, ix_lim=8, iy_lim=6, wf=1,
+          multi_infl=1.1, rtps=(0, 0.95),
+          types=[T(0, 11, 30, 50.0, 3.0, 100, **gts5),
+                 T(1, 2, 600, 12.0, 3.0, 300, err_muti=1.0, err_rej=8.0)])),
+        # 2-D family (gpspw alone) + radar kdp in the other family
+        ("driver_2d.npz", 404, dict(k=12, nx=9, ny=9, nz=4, ix_lim=9, iy_lim=9,
+          rtpp=(0, 0.95),
+          types=[T(0, 8, 40, 75.0, -1.0, 20, err_muti=0.5, upper=False),
+                 T(1, 4, 200, 24.0, 3.0, 300, err_muti=1.0, err_rej=8.0)])),
+        # Q1 defined case: last GTS type appended is 2-D (gpspw) -> 3-D types searched in 2-D
+        ("driver_q1.npz", 405, dict(k=10, nx=7, ny=8, nz=4, ix_lim=7, iy_lim=8,
+          types=[T(0, 2, 30, 50.0, 3.0, 100, **gts5),
+                 T(0, 8, 20, 75.0, -1.0, 20, err_muti=0.5, upper=False)])),
+        # offset state (xb ~ 285): fp32 rounding of the analysis at T-like magnitudes
+        ("driver_offset.npz", 406, dict(k=40, nx=9, ny=8, nz=5, ix_lim=9, iy_lim=8,
+          xb_mu=285.0, types=[T(1, 2, 700, 12.0, 3.0, 1000, err_muti=1.0, err_rej=8.0)])),
+        # radar zdr (type 3, 'MD', module_radar.f90:70-79) beside dbz with its norain rules
+        # and a sounding, k = 20, RTPS only
+        ("driver_zdr.npz", 407, dict(k=20, nx=10, ny=9, nz=5, ix_lim=10, iy_lim=9,
+          rtpp=(0, 0.95), multi_infl=1.3,
+          types=[T(0, 1, 25, 75.0, 3.0, 40, err_muti=[0.5, 0.5, 0.7, 0.5, 0.5]),
+                 T(1, 1, 300, 10.0, 2.0, 60, err_muti=2.5, err_rej=20.0),
+                 T(1, 3, 400, 12.0, 3.0, 200, err_muti=1.0, err_rej=6.0)])),
+    ]
+
+
+def main_driver(name):
+    """Regenerate one G4 case (and its manifest entry) without touching the others."""
+    case = [c for c in driver_cases() if c[0] == name]
+    if not case:
+        sys.exit(f"no driver case {name}")
+    fn, seed, kw = case[0]
+    d = gen_driver(fn, seed, **kw)
+    np.savez_compressed(os.path.join(OUT, fn), **d)
+    mf = os.path.join(OUT, "MANIFEST.json")
+    with open(mf) as f:
+        manifest = json.load(f)
+    manifest["files"][fn] = {"what": "G4 one variable through the driver loop", "seed": seed,
+                             "k": kw["k"], "grid": [kw["nx"], kw["ny"], kw["nz"]],
+                             "points_changed": int(np.any(d["var_out"] != d["var_in"], axis=0).sum())}
+    with open(mf, "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+    print(fn, manifest["files"][fn])
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build oracle/_ref/ref_harness first (make -C oracle ref)")
@@ -332,36 +391,7 @@ def main():
     np.savez_compressed(os.path.join(OUT, "gc.npz"), x=xs, y=gy)
     manifest["files"]["gc.npz"] = {"what": "G3 Gaspari_Cohn_1999"}
 
-    gts5 = dict(err_muti=[0.5] * 5, err_rej=[5.0] * 5)
-    drivers = [
-        # C1: 10x10x5, k=8, 50 synop obs at the surface (BASELINE.json configs[0])
-        ("driver_c1.npz", 401, dict(k=8, nx=10, ny=10, nz=5, ix_lim=10, iy_lim=10,
-          types=[T(0, 2, 50, 50.0, 3.0, 100, upper=False, **gts5)], ztop=6e3)),
-        # mixed GTS + radar, truncation (max_lz small), QC/gross/norain rejects, Q2 bounds
-        ("driver_mixed.npz", 402, dict(k=16, nx=12, ny=9, nz=6, ix_lim=11, iy_lim=9,
-          types=[T(0, 1, 30, 75.0, 3.0, 12, err_muti=[0.5, 0.5, 0.7, 0.5, 0.5]),
-                 T(0, 2, 40, 50.0, 3.0, 100, upper=False, is_assim=[1, 1, 0, 1, 1], **gts5),
-                 T(0, 10, 25, 50.0, 3.0, 9, **gts5),
-                 T(1, 1, 400, 8.0, 2.0, 30, err_muti=2.5, err_rej=20.0),
-                 T(1, 2, 500, 12.0, 3.0, 300, err_muti=1.0, err_rej=8.0)])),
-        # Gaspari-Cohn weighting, k = 40
-        ("driver_gc_k40.npz", 403, dict(k=40, nx=8, ny=7, nz=5, ix_lim=8, iy_lim=6, wf=1,
-          multi_infl=1.1, rtps=(0, 0.95),
-          types=[T(0, 11, 30, 50.0, 3.0, 100, **gts5),
-                 T(1, 2, 600, 12.0, 3.0, 300, err_muti=1.0, err_rej=8.0)])),
-        # 2-D family (gpspw alone) + radar kdp in the other family
-        ("driver_2d.npz", 404, dict(k=12, nx=9, ny=9, nz=4, ix_lim=9, iy_lim=9,
-          rtpp=(0, 0.95),
-          types=[T(0, 8, 40, 75.0, -1.0, 20, err_muti=0.5, upper=False),
-                 T(1, 4, 200, 24.0, 3.0, 300, err_muti=1.0, err_rej=8.0)])),
-        # Q1 defined case: last GTS type appended is 2-D (gpspw) -> 3-D types searched in 2-D
-        ("driver_q1.npz", 405, dict(k=10, nx=7, ny=8, nz=4, ix_lim=7, iy_lim=8,
-          types=[T(0, 2, 30, 50.0, 3.0, 100, **gts5),
-                 T(0, 8, 20, 75.0, -1.0, 20, err_muti=0.5, upper=False)])),
-        # offset state (xb ~ 285): fp32 rounding of the analysis at T-like magnitudes
-        ("driver_offset.npz", 406, dict(k=40, nx=9, ny=8, nz=5, ix_lim=9, iy_lim=8,
-          xb_mu=285.0, types=[T(1, 2, 700, 12.0, 3.0, 1000, err_muti=1.0, err_rej=8.0)])),
-    ]
+    drivers = driver_cases()
     for (fn, seed, kw) in drivers:
         d = gen_driver(fn, seed, **kw)
         np.savez_compressed(os.path.join(OUT, fn), **d)
@@ -380,6 +410,8 @@ if __name__ == "__main__":
         main_tuneq()
     elif sys.argv[1:] == ["dims"]:
         main_dims()
+    elif sys.argv[1:2] == ["driver"]:
+        main_driver(sys.argv[2])
     else:
         main()
         main_tuneq()

@@ -138,7 +138,7 @@ def test_search_matches_reference_order(name):
 
 
 DRIVERS = ["driver_c1.npz", "driver_mixed.npz", "driver_gc_k40.npz", "driver_2d.npz",
-           "driver_q1.npz", "driver_offset.npz"]
+           "driver_q1.npz", "driver_offset.npz", "driver_zdr.npz"]
 
 
 @pytest.mark.parametrize("name", DRIVERS)

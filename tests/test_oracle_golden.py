@@ -94,7 +94,7 @@ def test_search_kat_traversal_order(name):
 
 
 DRIVERS = ["driver_c1.npz", "driver_mixed.npz", "driver_gc_k40.npz", "driver_2d.npz",
-           "driver_q1.npz", "driver_offset.npz"]
+           "driver_q1.npz", "driver_offset.npz", "driver_zdr.npz"]
 
 
 @pytest.mark.parametrize("name", DRIVERS)
