@@ -256,11 +256,27 @@ __device__ __forceinline__ float slot_r2(const f32x4 d, int dim, float q0, float
 // products of the fp32 values stay exact in fp64 either way).
 // PITCH > KP (the matrix-core assembly): a staged column also holds yo in row KP and zeros
 // in rows KP+1 .. PITCH-1, so the MFMA operand rows [Yb; yo; 0] read without selects.
-template <int KP, int CHUNK, class E = float, int PITCH = KP>
+// SWZ (matrix-core pitches with PITCH % 32 == 16): column s starts 2 (s >> 1) words after
+// s * PITCH.  The pair staging's 8-byte stores (16 lanes = 16 columns at one row offset) then
+// hit 16 distinct bank pairs instead of 2 (8-way conflicts: ~2.6 k extra LDS cycles per
+// point), and the MFMA operand reads, whose two 32-lane groups read columns 4g, 4g + 1 and
+// 4g + 2, 4g + 3 (same shift, bases 16 banks apart), stay conflict-free.  Columns keep all
+// PITCH rows (the shifts grow with s), so the chunk takes CHUNK more words.
+template <int KP, int CHUNK, class E = float, int PITCH = KP, bool SWZ = false>
 struct ColumnChunk {
   E yb[CHUNK][PITCH];
+  E yb_shift[SWZ ? CHUNK : 1];  // room for the shifted columns (SWZ)
   E yo[CHUNK];
   unsigned long long expt[32];  // expf table (kExpT) in LDS: per-lane lookups stay on chip
+  // col(s + 4) = col(s) + GSTRIDE: the MFMA group loops step from col(kk) by it, so that the
+  // compiler sees one base and immediate offsets
+  static constexpr int GSTRIDE = 4 * PITCH + (SWZ ? 4 : 0);
+  __device__ __forceinline__ E *col(int s) {
+    return reinterpret_cast<E *>(this) + s * PITCH + (SWZ ? 2 * (s >> 1) : 0);
+  }
+  __device__ __forceinline__ const E *col(int s) const {
+    return reinterpret_cast<const E *>(this) + s * PITCH + (SWZ ? 2 * (s >> 1) : 0);
+  }
 };
 
 template <int KP, int NT = 64>
@@ -275,9 +291,9 @@ struct AsmLayout {
 // accumulate(nsl) on each staged chunk.  NT threads per point (`lane` = thread index).
 // Returns the number of accepted columns (p); with NT > 64 the count is valid in wave 0.
 template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64, class E = float, int PITCH = KP,
-          class Acc>
+          bool SWZ = false, class Acc>
 __device__ __forceinline__ int stage_columns(
-    ColumnChunk<KP, CHUNK, E, PITCH> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
+    ColumnChunk<KP, CHUNK, E, PITCH, SWZ> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
     const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in, Acc &&accumulate) {
@@ -287,7 +303,7 @@ __device__ __forceinline__ int stage_columns(
     if (lane < 32) ch.expt[lane] = kExpT[lane];
     if constexpr (PITCH > KP + 1) {  // rows KP+1 .. PITCH-1 of every column stay zero
       constexpr int NZ = PITCH - KP - 1;
-      for (int e = lane; e < CHUNK * NZ; e += NT) ch.yb[e / NZ][KP + 1 + e % NZ] = (E)0.0f;
+      for (int e = lane; e < CHUNK * NZ; e += NT) ch.col(e / NZ)[KP + 1 + e % NZ] = (E)0.0f;
     }
     // other waves read the table before the chunk loop's first barrier (error_inv below);
     // LDS is not cleared between workgroups, so without this they can read a previous
@@ -375,9 +391,9 @@ __device__ __forceinline__ int stage_columns(
         ptot += __popcll(__ballot(ok && half == 0));  // counted by wave 0
         if (half == 0) {
           ch.yo[sl] = (E)yo;
-          if constexpr (PITCH > KP) ch.yb[sl][KP] = (E)yo;
+          if constexpr (PITCH > KP) ch.col(sl)[KP] = (E)yo;
         }
-        E *dst = &ch.yb[sl][2 * VH * half];
+        E *dst = ch.col(sl) + 2 * VH * half;
 #pragma unroll
         for (int i = 0; i < VH; ++i) {
           // bg * error_inv (:452); w = 0 zeroes a rejected column and a lane past nsl (its
@@ -408,7 +424,7 @@ __device__ __forceinline__ int stage_columns(
           if (m < k) v = (E)yb_in[(c0 + base + s) * k + m];
           else if (m == KP) v = (E)yo_in[c0 + base + s];  // PITCH > KP only
         }
-        ch.yb[s][m] = v;
+        ch.col(s)[m] = v;
       }
       __syncthreads();
       accumulate(nsl);
@@ -434,9 +450,9 @@ __device__ __forceinline__ float other_half(float x, int half) {
 // weight) and stages half `half` of the bg row of column sl of chunk c, then of chunk c + 1;
 // the weight of the column it stages but does not own comes from lane sl + 32 (half 0) or
 // sl (half 1) by one swap.  Same columns, order and arithmetic as stage_columns.
-template <int KP, int CHUNK, int PITCH, class Acc>
+template <int KP, int CHUNK, int PITCH, bool SWZ, class Acc>
 __device__ __forceinline__ int stage_columns_pair(
-    ColumnChunk<KP, CHUNK, float, PITCH> &ch, const TreeDesc *__restrict__ trees,
+    ColumnChunk<KP, CHUNK, float, PITCH, SWZ> &ch, const TreeDesc *__restrict__ trees,
     const SolveConsts &c, int gi, int lane, const int *__restrict__ nbr_cnt,
     const int *__restrict__ nbr_idx, const float3 pt, Acc &&accumulate) {
   static_assert(CHUNK == 32, "two lanes per staged column");
@@ -446,7 +462,7 @@ __device__ __forceinline__ int stage_columns_pair(
   if (lane < 32) ch.expt[lane] = kExpT[lane];
   if constexpr (PITCH > KP + 1) {
     constexpr int NZ = PITCH - KP - 1;
-    for (int e = lane; e < CHUNK * NZ; e += 64) ch.yb[e / NZ][KP + 1 + e % NZ] = 0.0f;
+    for (int e = lane; e < CHUNK * NZ; e += 64) ch.col(e / NZ)[KP + 1 + e % NZ] = 0.0f;
   }
   const int sl = lane % CHUNK, half = lane / CHUNK;
   for (int t = 0; t < c.ntrees; ++t) {
@@ -476,7 +492,7 @@ __device__ __forceinline__ int stage_columns_pair(
       for (int i = 0; i < VH / 2; ++i) g[i] = gld4(T.col_bg, b0 + 4u * i);
     };
     auto put = [&](const f32x4 (&g)[VH / 2], float w) {  // bg * error_inv (:452)
-      float *d = &ch.yb[sl][2 * VH * half];
+      float *d = ch.col(sl) + 2 * VH * half;
 #pragma unroll
       for (int i = 0; i < VH / 2; ++i) {
         *reinterpret_cast<float2 *>(d + 4 * i) = make_float2(g[i].x * w, g[i].y * w);
@@ -511,7 +527,7 @@ __device__ __forceinline__ int stage_columns_pair(
       const float w_b = half ? w : w_x;
       if (half == 0) {
         ch.yo[sl] = yo;
-        if constexpr (PITCH > KP) ch.yb[sl][KP] = yo;
+        if constexpr (PITCH > KP) ch.col(sl)[KP] = yo;
       }
       put(g, half ? w_x : w);
       const bool two = base + CHUNK < npairs;  // wave-uniform
@@ -522,7 +538,7 @@ __device__ __forceinline__ int stage_columns_pair(
       if (two) {
         if (half == 1) {
           ch.yo[sl] = yo;
-          if constexpr (PITCH > KP) ch.yb[sl][KP] = yo;
+          if constexpr (PITCH > KP) ch.col(sl)[KP] = yo;
         }
         put(g, w_b);
         __syncthreads();
@@ -714,13 +730,15 @@ struct MfmaLayout {
   static constexpr bool YO_ROW = KP + 1 <= 16 * NT;      // yo rides in the padding
   static constexpr int NTL = NT * (NT + 1) / 2;          // lower tiles
   static constexpr int PITCH = YO_ROW ? 16 * NT : KP;    // staged column length
+  static constexpr bool SWZ = PITCH % 32 == 16;          // shifted columns (ColumnChunk)
   static constexpr int NBL4 = YO_ROW ? (KP + 1 - 16 * (NT - 1) + 3) / 4 : 4;  // live strips
   static constexpr bool SPLIT_LAST = NBL4 < 4;
 };
 
 template <int KP, int CHUNK, bool ASSEMBLED>
 __device__ __forceinline__ void assemble_point_mfma(
-    ColumnChunk<KP, CHUNK, float, MfmaLayout<KP>::PITCH> &ch, const TreeDesc *__restrict__ trees,
+    ColumnChunk<KP, CHUNK, float, MfmaLayout<KP>::PITCH, MfmaLayout<KP>::SWZ> &ch,
+    const TreeDesc *__restrict__ trees,
     const SolveConsts &c, int gi, int lane, const int *__restrict__ nbr_cnt,
     const int *__restrict__ nbr_idx, const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in,
@@ -732,8 +750,8 @@ __device__ __forceinline__ void assemble_point_mfma(
   const int kk = lane >> 4, m = lane & 15;
   auto stage = [&](auto &&acc) {
     if constexpr (!ASSEMBLED && CHUNK == 32)
-      return stage_columns_pair<KP, CHUNK, MfmaLayout<KP>::PITCH>(ch, trees, c, gi, lane, nbr_cnt,
-                                                                  nbr_idx, pt, acc);
+      return stage_columns_pair<KP, CHUNK, MfmaLayout<KP>::PITCH, MfmaLayout<KP>::SWZ>(
+          ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, acc);
     else
       return stage_columns<KP, CHUNK, ASSEMBLED>(ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt,
                                                  col_off, yo_in, yb_in, acc);
@@ -748,21 +766,23 @@ __device__ __forceinline__ void assemble_point_mfma(
         static_assert(CHUNK % 4 == 0, "k-slots");
         constexpr int NS = L::SPLIT_LAST ? L::NBL4 : 1;
         float f[2][L::NT], fy[2], fs[2][NS];
-        auto load = [&](int b, int s) {
+        const float *c0 = ch.col(kk);  // column 4 g + kk at c0 + g GSTRIDE
+        auto load = [&](int b, int g) {
+          const float *cs = c0 + g * ch.GSTRIDE;
 #pragma unroll
           for (int I = 0; I < L::NT; ++I) {
             const int row = 16 * I + m;
-            if constexpr (L::YO_ROW) f[b][I] = ch.yb[s][row];
-            else f[b][I] = ch.yb[s][row < KP ? row : KP - 1];
+            if constexpr (L::YO_ROW) f[b][I] = cs[row];
+            else f[b][I] = cs[row < KP ? row : KP - 1];
           }
           if constexpr (L::SPLIT_LAST) {  // strip rows, broadcast over the 4 blocks
 #pragma unroll
-            for (int r = 0; r < NS; ++r) fs[b][r] = ch.yb[s][16 * (L::NT - 1) + 4 * r + (m & 3)];
+            for (int r = 0; r < NS; ++r) fs[b][r] = cs[16 * (L::NT - 1) + 4 * r + (m & 3)];
           }
-          if constexpr (!L::YO_ROW) fy[b] = ch.yo[s];
+          if constexpr (!L::YO_ROW) fy[b] = ch.yo[4 * g + kk];
         };
         const int nl = c.debug_stop == 11 ? 0 : nsl;
-        if (nl > 0) load(0, kk);
+        if (nl > 0) load(0, 0);
 #pragma unroll
         for (int g = 0; g < CHUNK / 4; ++g) {
           if (4 * g >= nl) break;  // nsl is wave-uniform
@@ -780,7 +800,7 @@ __device__ __forceinline__ void assemble_point_mfma(
           double os[NS];
 #pragma unroll
           for (int r = 0; r < NS; ++r) os[r] = L::SPLIT_LAST ? (double)fs[b][r] : 0.0;
-          if (g + 1 < CHUNK / 4 && 4 * (g + 1) < nl) load(b ^ 1, 4 * (g + 1) + kk);
+          if (g + 1 < CHUNK / 4 && 4 * (g + 1) < nl) load(b ^ 1, g + 1);
           int t = 0;
 #pragma unroll
           for (int I = 0; I < L::NT; ++I)
@@ -797,7 +817,7 @@ __device__ __forceinline__ void assemble_point_mfma(
         }
         if constexpr (!L::YO_ROW) {
           for (int s = 0; s < nsl; ++s)
-            if (lane < KP) b1acc = fma((double)ch.yb[s][lane], (double)ch.yo[s], b1acc);
+            if (lane < KP) b1acc = fma((double)ch.col(s)[lane], (double)ch.yo[s], b1acc);
         }
       });
 }

@@ -79,7 +79,8 @@ struct TqSmem {
   static constexpr int pb_base(int J) { return REG - (NB - J) * PLD; }
   static constexpr int pb2_base(int J2) { return REG - (NB2 - J2) * PLD2; }
   union {
-    ColumnChunk<KP, kTqChunk, TqStage, kTqMfmaAssembly ? MfmaLayout<KP>::PITCH : KP> ch;
+    ColumnChunk<KP, kTqChunk, TqStage, kTqMfmaAssembly ? MfmaLayout<KP>::PITCH : KP,
+                kTqMfmaAssembly && MfmaLayout<KP>::SWZ> ch;
     double ah[KP / 2][KP + 2];            // half of A on its way from MFMA tiles to blocks
     double reg[REG];                      // hv[0, NHV) | y after the loop | pb
   } u;
@@ -673,7 +674,7 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   constexpr int KP = kTq4KP, PITCH = 48, YO = KP;
   static_assert(KP == 40 && MfmaLayout<KP>::PITCH == PITCH, "the cover is laid out for KP = 40");
   using HO = AsmRecord<KP>;
-  __shared__ ColumnChunk<KP, kTqChunk, float, PITCH> ch;
+  __shared__ ColumnChunk<KP, kTqChunk, float, PITCH, true> ch;  // shifted columns (SWZ)
   const int gi = xcd_remap(blockIdx.x, gridDim.x);
   if (gi >= npts) return;
   const int lane = threadIdx.x, kk = lane >> 4, m = lane & 15;
@@ -689,6 +690,9 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   constexpr int kRowA[16] = {32, 33, 34, 35, 36, 37, 38, 39, 36, 37, 38, 39, 35, 39, 0, 16};
   constexpr int kColB[16] = {YO, 32, 33, 34, YO, 35, 36, 37, 32, 33, 34, 38, 35, 39, 0, 16};
   const int ra = pick(kRowA, m), cb = pick(kColB, m);
+  // A rows of the diagonal tiles: yo in place of rows 0 and 16 (read from the staged yo row,
+  // not selected after the conversion: 2 reads instead of 4 v_cndmask per group)
+  const int r0 = m == 0 ? YO : m, r1 = m == 0 ? YO : 16 + m;
   f64x4 t0 = {0.0, 0.0, 0.0, 0.0}, t1 = t0, t2 = t0;
   double st[4] = {0.0, 0.0, 0.0, 0.0}, cn = 0.0;
   const int ptot = stage_columns_pair<KP, kTqChunk, PITCH>(
@@ -696,28 +700,30 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
         // column s = 4 g + kk of the chunk is k-slot kk of group g; staged columns past nsl
         // are zero.  The group loop is unrolled with a static double buffer: group g + 1's
         // operands are read before group g's MFMAs.
-        float f[2][7];
-        auto load = [&](int b, int sc) {
-          const float *col = ch.yb[sc];
+        float f[2][8];
+        const float *c0 = ch.col(kk);  // column 4 g + kk at c0 + g GSTRIDE
+        auto load = [&](int b, int g) {
+          const float *col = c0 + g * ch.GSTRIDE;
           f[b][0] = col[m];
           f[b][1] = col[16 + m];
-          f[b][2] = col[YO];
+          f[b][2] = col[r0];
           f[b][3] = col[32 + (m & 3)];
           f[b][4] = col[36 + (m & 3)];
           f[b][5] = col[ra];
           f[b][6] = col[cb];
+          f[b][7] = col[r1];
         };
         const int nl = c.debug_stop == 11 ? 0 : nsl;
-        if (nl > 0) load(0, kk);
+        if (nl > 0) load(0, 0);
 #pragma unroll
         for (int g = 0; g < kTqChunk / 4; ++g) {
           if (4 * g >= nl) break;  // nsl is wave-uniform
           const int b = g & 1;
-          const double o0 = (double)f[b][0], o1 = (double)f[b][1], oy = (double)f[b][2];
-          const double a0 = m == 0 ? oy : o0, a1 = m == 0 ? oy : o1;
+          const double o0 = (double)f[b][0], o1 = (double)f[b][1];
+          const double a0 = (double)f[b][2], a1 = (double)f[b][7];
           const double s0 = (double)f[b][3], s1 = (double)f[b][4];
           const double ca = (double)f[b][5], cbv = (double)f[b][6];
-          if (g + 1 < kTqChunk / 4 && 4 * (g + 1) < nl) load(b ^ 1, 4 * (g + 1) + kk);
+          if (g + 1 < kTqChunk / 4 && 4 * (g + 1) < nl) load(b ^ 1, g + 1);
           t0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, o0, t0, 0, 0, 0);
           t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(o1, o0, t1, 0, 0, 0);
           t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, o1, t2, 0, 0, 0);
