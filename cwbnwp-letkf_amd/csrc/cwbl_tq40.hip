@@ -58,6 +58,26 @@ __device__ __forceinline__ float rbcast(float x) {
 // value of lane l ^ 8 of the row (row_ror:8)
 __device__ __forceinline__ double ror8(double x) { return dpp_f64<0x128>(x); }
 
+// acc + x_L y and acc - x_L y, x_L = lane L of this lane's 16-lane row: one v_fmac_f64_dpp
+// row_newbcast (gfx950's 64-bit DPP) instead of a v_mov_b64_dpp broadcast and an FMA.  The
+// compiler does not form it itself (its DPP combine sees the three-address v_fma_f64).  A
+// DPP source must not be written by the VALU in the two instructions before; the steps write
+// their sources once and pin them behind an s_nop 1 (dpp_pin) before the first use, and the
+// compiler's hazard check covers the inline asm's other operands.
+template <int L>
+__device__ __forceinline__ double fmac_row(double acc, double x, double y) {
+  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "+v"(acc) : "v"(x), "v"(y), "i"(L));
+  return acc;
+}
+template <int L>
+__device__ __forceinline__ double fnmac_row(double acc, double x, double y) {
+  asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "+v"(acc) : "v"(x), "v"(y), "i"(L));
+  return acc;
+}
+__device__ __forceinline__ void dpp_pin(double &x) { asm volatile("s_nop 1" : "+v"(x)); }
+
 }  // namespace
 
 template <int KP>
@@ -246,25 +266,30 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       ux[r] = fma(-tau * s2, v[r], ux[r]);
       ub[r] = fma(-tau * s3, v[r], ub[r]);
     });
-    // v_c of column c, wave-uniform per row: prefix lane c (c < J0) or its slot lane
-    auto vcol_of = [&](auto cc, const double &vp, const double (&vs)[NS]) {
+    // v_c of column c, wave-uniform per row: prefix lane c (c < J0) or its slot lane; the
+    // products with it are one fmac_row each (acc + v_c y)
+    auto src_of = [&](auto cc, const double &vp, const double (&vs)[NS]) -> const double & {
       constexpr int col = decltype(cc)::value;
-      if constexpr (col < J0) return rbcast<col>(vp);
-      else return rbcast<(col - J0) % 16>(vs[(col - J0) / 16]);
+      if constexpr (col < J0) return vp;
+      else return vs[(col - J0) / 16];
     };
+    auto lane_of = [](int col) { return col < J0 ? col : (col - J0) % 16; };
+    dpp_pin(vP);
+    sfor<NS>([&](auto rr) { dpp_pin(v[decltype(rr)::value]); });
     // A v: slot rows over columns j+1 .. KP-1; prefix rows = their block part + the column
     // sums over the slot rows (A(i, c) = A(c, i) for c >= J0)
     double p0[NS], p1[NS], pP = 0.0;
     sfor<NS>([&](auto rr) { p0[decltype(rr)::value] = p1[decltype(rr)::value] = 0.0; });
     sfor<KP - J1>([&](auto cc) {
       constexpr int col = J1 + decltype(cc)::value;
-      const double vc = vcol_of(std::integral_constant<int, col>{}, vP, v);
+      constexpr int LC = lane_of(col);
+      const double &vs = src_of(std::integral_constant<int, col>{}, vP, v);
       sfor<NS>([&](auto rr) {
         constexpr int r = decltype(rr)::value;
-        if constexpr ((col - J1) % 2 == 0) p0[r] = fma(A[r][col], vc, p0[r]);
-        else p1[r] = fma(A[r][col], vc, p1[r]);
+        if constexpr ((col - J1) % 2 == 0) p0[r] = fmac_row<LC>(p0[r], vs, A[r][col]);
+        else p1[r] = fmac_row<LC>(p1[r], vs, A[r][col]);
       });
-      if constexpr (col < J0) pP = fma(Pb[col], vc, pP);
+      if constexpr (col < J0) pP = fmac_row<LC>(pP, vs, Pb[col]);
     });
     sfor<J0 - J1>([&](auto cc) {  // prefix rows j+1 .. J0-1: column sums of the slots
       constexpr int col = J1 + decltype(cc)::value;
@@ -292,18 +317,20 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     // A <- A - v w^T - w v^T: slot rows over columns j+1 .. KP-1, the prefix block over
     // columns j+1 .. J0-1.  (v is renamed first: otherwise the compiler reuses the matvec's
     // broadcasts and keeps all KP - j of them live across the reduction, which spills.)
-    asm volatile("" : "+v"(vP));
-#pragma unroll
-    for (int r = 0; r < NS; ++r) asm volatile("" : "+v"(v[r]));
+    double wPp = wP;
+    dpp_pin(wPp);
+    sfor<NS>([&](auto rr) { dpp_pin(wv[decltype(rr)::value]); });
     sfor<KP - J1>([&](auto cc) {
       constexpr int col = J1 + decltype(cc)::value;
-      const double vc = vcol_of(std::integral_constant<int, col>{}, vP, v);
-      const double wc = vcol_of(std::integral_constant<int, col>{}, wP, wv);
+      constexpr int LC = lane_of(col);
+      const double &vs = src_of(std::integral_constant<int, col>{}, vP, v);
+      const double &ws = src_of(std::integral_constant<int, col>{}, wPp, wv);
       sfor<NS>([&](auto rr) {
         constexpr int r = decltype(rr)::value;
-        A[r][col] = fma(-v[r], wc, fma(-wv[r], vc, A[r][col]));
+        // A - wv v_c - v w_c, in this order
+        A[r][col] = fnmac_row<LC>(fnmac_row<LC>(A[r][col], vs, wv[r]), ws, v[r]);
       });
-      if constexpr (col < J0) Pb[col] = fma(-vP, wc, fma(-wP, vc, Pb[col]));
+      if constexpr (col < J0) Pb[col] = fnmac_row<LC>(fnmac_row<LC>(Pb[col], vs, wPp), ws, vP);
     });
   });
   // a (one-wave) workgroup barrier: a fence the scheduler does not move phase 2 across
@@ -369,14 +396,14 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       // that one broadcast v_c is live at a time
       double p0[NS], p1[NS];
       sfor<NS>([&](auto rr) { p0[decltype(rr)::value] = p1[decltype(rr)::value] = 0.0; });
+      sfor<NS>([&](auto rr) { dpp_pin(v[decltype(rr)::value]); });
       sfor<KT - J1>([&](auto cc) {
         constexpr int cl = J1 + decltype(cc)::value;
-        const double vcol = rbcast<cl % 16>(v[cl / 16]);
         sfor<NS>([&](auto rr) {
           constexpr int r = decltype(rr)::value;
           if constexpr (16 * r + 15 > jl) {
-            if constexpr ((cl - J1) % 2 == 0) p0[r] = fma(A[r][J0 + cl], vcol, p0[r]);
-            else p1[r] = fma(A[r][J0 + cl], vcol, p1[r]);
+            if constexpr ((cl - J1) % 2 == 0) p0[r] = fmac_row<cl % 16>(p0[r], v[cl / 16], A[r][J0 + cl]);
+            else p1[r] = fmac_row<cl % 16>(p1[r], v[cl / 16], A[r][J0 + cl]);
           }
         });
       });
@@ -393,17 +420,15 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         const int t = l + 16 * r;
         wv[r] = t > jl ? fma(-0.5 * tau * s1, v[r], tau * pp[r]) : 0.0;
       });
-      // A <- A - v w^T - w v^T on the trailing rows and columns (v renamed: fresh broadcasts)
-#pragma unroll
-      for (int r = 0; r < NS; ++r) asm volatile("" : "+v"(v[r]));
+      // A <- A - v w^T - w v^T on the trailing rows and columns
+      sfor<NS>([&](auto rr) { dpp_pin(wv[decltype(rr)::value]); });
       sfor<KT - J1>([&](auto cc) {
         constexpr int cl = J1 + decltype(cc)::value;
-        const double vcol = rbcast<cl % 16>(v[cl / 16]);
-        const double wcol = rbcast<cl % 16>(wv[cl / 16]);
         sfor<NS>([&](auto rr) {
           constexpr int r = decltype(rr)::value;
           if constexpr (16 * r + 15 > jl)
-            A[r][J0 + cl] = fma(-v[r], wcol, fma(-wv[r], vcol, A[r][J0 + cl]));
+            A[r][J0 + cl] =
+                fnmac_row<cl % 16>(fnmac_row<cl % 16>(A[r][J0 + cl], v[cl / 16], wv[r]), wv[cl / 16], v[r]);
         });
       });
     } else {  // the trailing 2x2: already tridiagonal (c(KP-2,KP-3) is step KP-3's beta)
