@@ -141,18 +141,15 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     xbl[vs] = mem ? xv : 0.0f;
   });
   // fp32 sum over members in member order; member m is row m: prefix slot lane m (m < J0),
-  // else row slot (m - J0) / 16, lane (m - J0) % 16
-  // (the member masks m < k are recomputed per call from an opaque copy of k: kept from the
-  // prologue to the epilogue they are 40 SGPR pairs, spilled to VGPR lanes)
+  // else row slot (m - J0) / 16, lane (m - J0) % 16.  Every caller's x is +0 on the rows past
+  // k, and s + 0 = s (s is never -0), so the rows past k need no mask and each term is one
+  // v_add_f32 with a row_newbcast source.
   auto seq_sum_f32 = [&](const float (&x)[NV]) {
-    int kk = k;
-    asm volatile("" : "+s"(kk));
     float s = 0.0f;
     sfor<KP>([&](auto mm) {
       constexpr int m = decltype(mm)::value;
       constexpr int vs = m < J0 ? 0 : 1 + (m - J0) / 16, ln = m < J0 ? m : (m - J0) % 16;
-      const float b = rbcast<ln>(x[vs]);
-      s = s + (m < kk ? b : 0.0f);  // s + 0 = s: s is never -0
+      s = s + rbcast<ln>(x[vs]);
     });
     return s;
   };
