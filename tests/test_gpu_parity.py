@@ -513,6 +513,39 @@ def test_dense_radar_c5_block_vs_oracle():
     assert rel <= INCR_TOL, rel
 
 
+def test_c5_full_size_properties():
+    """C5 at its stated size on one GPU (600x600x60 = 21.6 M points, k=40, 1.66 M dense
+    radar obs, max_lz 4000; the configuration names 8 GPUs, whose rank shares are column
+    blocks of this grid): finite, no non-convergence, run-to-run bitwise reproducible, and
+    the oracle on a column block in the dense centre."""
+    import ctypes as C
+    from cwbl import synth
+    w = synth.make("c5")
+    c = core(w.k)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    var = w.var.copy()
+    st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+    assert st.points == w.points
+    assert np.isfinite(var).all()
+    assert st.nonconverged == 0
+    mean_p = st.nobs_sum / max(st.solved, 1)
+    assert 600 <= mean_p <= 4000, mean_p
+    var2 = w.var.copy()
+    c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var2))
+    np.testing.assert_array_equal(var.view(np.uint32), var2.view(np.uint32))
+    del var2
+    j0, i0, nb = 297, 297, 4
+    sub = lambda a: np.ascontiguousarray(a[..., j0:j0 + nb, i0:i0 + nb])  # noqa: E731
+    ref = sub(w.var).copy()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(sub(w.x), sub(w.y), sub(w.alt), ref)),
+                                  16, C.byref(abi.Stats()))
+    assert rc == 0
+    rel = increment_rel_rms(sub(var), ref, sub(w.var))
+    assert rel <= INCR_TOL, rel
+
+
 @pytest.mark.parametrize("k", [80, 100, 128])
 def test_large_ensemble_block_vs_oracle(k):
     """configs[3]-shaped large ensembles (k = 128, and k = 80 on the KP = 96 kernel) on a
