@@ -262,7 +262,13 @@ __device__ __forceinline__ float slot_r2(const f32x4 d, int dim, float q0, float
 // point), and the MFMA operand reads, whose two 32-lane groups read columns 4g, 4g + 1 and
 // 4g + 2, 4g + 3 (same shift, bases 16 banks apart), stay conflict-free.  Columns keep all
 // PITCH rows (the shifts grow with s), so the chunk takes CHUNK more words.
-template <int KP, int CHUNK, class E = float, int PITCH = KP, bool SWZ = false>
+//
+// XSW (the 256-thread kernels' chunks, PITCH = 128): row r of an odd column is stored at
+// r ^ 16.  Their MFMA operand reads (two 32-lane groups, columns 4g + kk, rows 16 x + m) then
+// put the odd column 16 banks away from the even one instead of on the same banks (2-way),
+// and with the staging stores' rotated order (stage_columns_pipe) the stores of 16 lanes
+// (16 columns) spread over the banks instead of all hitting one (16-way); no extra LDS.
+template <int KP, int CHUNK, class E = float, int PITCH = KP, bool SWZ = false, bool XSW = false>
 struct ColumnChunk {
   E yb[CHUNK][PITCH];
   E yb_shift[SWZ ? CHUNK : 1];  // room for the shifted columns (SWZ)
@@ -277,6 +283,9 @@ struct ColumnChunk {
   __device__ __forceinline__ const E *col(int s) const {
     return reinterpret_cast<const E *>(this) + s * PITCH + (SWZ ? 2 * (s >> 1) : 0);
   }
+  static __device__ __forceinline__ int xr(int s) { return XSW ? 16 * (s & 1) : 0; }
+  __device__ __forceinline__ E &at(int s, int row) { return col(s)[row ^ xr(s)]; }
+  __device__ __forceinline__ const E &at(int s, int row) const { return col(s)[row ^ xr(s)]; }
 };
 
 template <int KP, int NT = 64>
@@ -291,9 +300,9 @@ struct AsmLayout {
 // accumulate(nsl) on each staged chunk.  NT threads per point (`lane` = thread index).
 // Returns the number of accepted columns (p); with NT > 64 the count is valid in wave 0.
 template <int KP, int CHUNK, bool ASSEMBLED, int NT = 64, class E = float, int PITCH = KP,
-          bool SWZ = false, class Acc>
+          bool SWZ = false, bool XSW = false, class Acc>
 __device__ __forceinline__ int stage_columns(
-    ColumnChunk<KP, CHUNK, E, PITCH, SWZ> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
+    ColumnChunk<KP, CHUNK, E, PITCH, SWZ, XSW> &ch, const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
     const float3 pt, const long long *__restrict__ col_off,
     const float *__restrict__ yo_in, const float *__restrict__ yb_in, Acc &&accumulate) {
@@ -303,7 +312,7 @@ __device__ __forceinline__ int stage_columns(
     if (lane < 32) ch.expt[lane] = kExpT[lane];
     if constexpr (PITCH > KP + 1) {  // rows KP+1 .. PITCH-1 of every column stay zero
       constexpr int NZ = PITCH - KP - 1;
-      for (int e = lane; e < CHUNK * NZ; e += NT) ch.col(e / NZ)[KP + 1 + e % NZ] = (E)0.0f;
+      for (int e = lane; e < CHUNK * NZ; e += NT) ch.at(e / NZ, KP + 1 + e % NZ) = (E)0.0f;
     }
     // other waves read the table before the chunk loop's first barrier (error_inv below);
     // LDS is not cleared between workgroups, so without this they can read a previous
@@ -391,18 +400,18 @@ __device__ __forceinline__ int stage_columns(
         ptot += __popcll(__ballot(ok && half == 0));  // counted by wave 0
         if (half == 0) {
           ch.yo[sl] = (E)yo;
-          if constexpr (PITCH > KP) ch.col(sl)[KP] = (E)yo;
+          if constexpr (PITCH > KP) ch.at(sl, KP) = (E)yo;
         }
-        E *dst = ch.col(sl) + 2 * VH * half;
 #pragma unroll
         for (int i = 0; i < VH; ++i) {
           // bg * error_inv (:452); w = 0 zeroes a rejected column and a lane past nsl (its
           // bg is a finite table entry of an earlier slot)
           const float y0 = g[i].x * w, y1 = g[i].y * w;
+          E *dst = &ch.at(sl, 2 * VH * half + 2 * i);  // (an aligned pair under XSW too)
           if constexpr (sizeof(E) == 8) {
-            *reinterpret_cast<double2 *>(dst + 2 * i) = make_double2((double)y0, (double)y1);
+            *reinterpret_cast<double2 *>(dst) = make_double2((double)y0, (double)y1);
           } else {
-            *reinterpret_cast<float2 *>(dst + 2 * i) = make_float2(y0, y1);
+            *reinterpret_cast<float2 *>(dst) = make_float2(y0, y1);
           }
         }
         __syncthreads();
@@ -424,7 +433,7 @@ __device__ __forceinline__ int stage_columns(
           if (m < k) v = (E)yb_in[(c0 + base + s) * k + m];
           else if (m == KP) v = (E)yo_in[c0 + base + s];  // PITCH > KP only
         }
-        ch.col(s)[m] = v;
+        ch.at(s, m) = v;
       }
       __syncthreads();
       accumulate(nsl);
@@ -555,9 +564,9 @@ __device__ __forceinline__ int stage_columns_pair(
 // LDS writes) to the other buffer after it, so their latency hides behind the matrix cores;
 // one barrier per chunk.  Same columns, order and arithmetic as stage_columns;
 // accumulate(nsl, chunk) reads the chunk to accumulate.
-template <int KP, int CHUNK, int NT, class Acc>
+template <int KP, int CHUNK, int NT, bool XSW, class Acc>
 __device__ __forceinline__ int stage_columns_pipe(
-    ColumnChunk<KP, CHUNK> (&ch)[2], const TreeDesc *__restrict__ trees, const SolveConsts &c,
+    ColumnChunk<KP, CHUNK, float, KP, false, XSW> (&ch)[2], const TreeDesc *__restrict__ trees, const SolveConsts &c,
     int gi, int lane, const int *__restrict__ nbr_cnt, const int *__restrict__ nbr_idx,
     const float3 pt, Acc &&accumulate) {
   static_assert(NT > 64 && NT % CHUNK == 0 && CHUNK <= 64, "threads per staged column");
@@ -568,6 +577,11 @@ __device__ __forceinline__ int stage_columns_pipe(
   if (lane < 32) ch[0].expt[lane] = kExpT[lane];
   __syncthreads();  // (LDS is not cleared between workgroups)
   const int sl = lane % CHUNK, half = lane / CHUNK;
+  // XSW: a thread gathers and stores its VH / 2 float4 of the bg row starting at float4
+  // (sl >> 1) mod VH / 2, so the 16 threads of a store group write 8 row offsets (with the
+  // odd columns' r ^ 16 on top) instead of one
+  static_assert(!XSW || ((VH / 2) & (VH / 2 - 1)) == 0, "rotation modulo a power of two");
+  const int rot = XSW ? (sl >> 1) & (VH / 2 - 1) : 0;
   int cur = 0;
   for (int t = 0; t < c.ntrees; ++t) {
     const TreeDesc T = trees[t];
@@ -603,13 +617,14 @@ __device__ __forceinline__ int stage_columns_pipe(
       const int col = slot * nvar + v;  // a valid table index even past the list (slot 0)
       const unsigned b0 = (unsigned)(col * KP + 2 * VH * half);
 #pragma unroll
-      for (int i = 0; i < VH / 2; ++i) G.g[i] = gld4(T.col_bg, b0 + 4u * i);
+      for (int i = 0; i < VH / 2; ++i)
+        G.g[i] = gld4(T.col_bg, b0 + 4u * (unsigned)((i + rot) & (VH / 2 - 1)));
       G.okb = gld(T.col_ok, (unsigned)col);
       G.err = gld(T.col_err, (unsigned)col);
       G.omm = gld(T.col_omm, (unsigned)col);
       G.rd = gld4(reinterpret_cast<const float *>(T.rdata), 4u * (unsigned)slot);
     };
-    auto commit = [&](const Gath &G, ColumnChunk<KP, CHUNK> &dst) {
+    auto commit = [&](const Gath &G, ColumnChunk<KP, CHUNK, float, KP, false, XSW> &dst) {
       // Every gathered register is consumed here, unconditionally: a dead component (rd.w)
       // would have its register reused at once, and a use the compiler sinks into a divergent
       // branch leaves the load pending on the skipping path; either way a later write to
@@ -624,11 +639,11 @@ __device__ __forceinline__ int stage_columns_pipe(
       const float yo = ok ? G.omm * wv : 0.0f;  // omm * error_inv (:451)
       ptot += __popcll(__ballot(ok && half == 0));  // counted by wave 0
       if (half == 0) dst.yo[sl] = yo;
-      float *d = &dst.yb[sl][2 * VH * half];
 #pragma unroll
       for (int i = 0; i < VH / 2; ++i) {  // bg * error_inv (:452)
-        *reinterpret_cast<float2 *>(d + 4 * i) = make_float2(G.g[i].x * w, G.g[i].y * w);
-        *reinterpret_cast<float2 *>(d + 4 * i + 2) = make_float2(G.g[i].z * w, G.g[i].w * w);
+        const int r = 2 * VH * half + 4 * ((i + rot) & (VH / 2 - 1));
+        *reinterpret_cast<float2 *>(&dst.at(sl, r)) = make_float2(G.g[i].x * w, G.g[i].y * w);
+        *reinterpret_cast<float2 *>(&dst.at(sl, r + 2)) = make_float2(G.g[i].z * w, G.g[i].w * w);
       }
     };
     int slot_n = slot_of(CHUNK);  // chunk 1's slots, loaded behind chunk 0's gathers

@@ -68,7 +68,8 @@ struct BigSmem {
   static constexpr int NB = KP / 4;
   static constexpr int PLD = 4 * NB + 4;  // 2*PLD = 8*odd dwords: conflict-free row sums
   union {
-    ColumnChunk<KP, kBigChunk<KP>> ch[2];     // staged columns (two buffers: stage_columns_pipe)
+    // staged columns (two buffers: stage_columns_pipe); odd columns' rows XOR 16 at KP = 128
+    ColumnChunk<KP, kBigChunk<KP>, float, KP, false, KP == 128> ch[2];
     double pb[NB][PLD];                   // A v partials: pb[R][4c+r] = block (R,c), row r
   } u;
   double col[KP];                         // pivot column / reflector j (back-transform)
@@ -206,15 +207,23 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     for (int t = 0; t < NTW; ++t) offJ[t] = 16 * (t <= wave ? t : t - wave - 1) + m;
     // columns past nsl are staged as zeros (a multiple of 4 stays inside the chunk)
     // (debug_stop 12: staging only, timing ablation)
-    auto mfma_chunk = [&](int nsl, const ColumnChunk<KP, kBigChunk<KP>> &cb) {
+    // the rows of column 4 g + kk are XOR 16 for odd kk (ColumnChunk XSW): the lane's offsets
+    // take it once
+    using CC = std::remove_reference_t<decltype(sm.u.ch[0])>;
+    const int xk = CC::xr(kk);
+    const int offAx = offA ^ xk, offBx = offB ^ xk;
+    int offJx[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) offJx[t] = offJ[t] ^ xk;
+    auto mfma_chunk = [&](int nsl, const CC &cb) {
       // (software-pipelining the group loop, group g + 1's operand reads before group g's
       // MFMAs, measured no faster: 2.52 s per C4 variable either way)
       for (int s0 = 0; s0 < (c.debug_stop == 12 ? 0 : nsl); s0 += 4) {
         const float *ys = cb.yb[s0 + kk];
-        const double a = (double)ys[offA], b = (double)ys[offB];
+        const double a = (double)ys[offAx], b = (double)ys[offBx];
 #pragma unroll
         for (int t = 0; t < NTW; ++t)
-          tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(t <= wave ? a : b, (double)ys[offJ[t]],
+          tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(t <= wave ? a : b, (double)ys[offJx[t]],
                                                          tile[t], 0, 0, 0);
       }
       // Yb d (row KP of [Yb; yo] does not fit the tile padding): eight columns per round,
@@ -228,7 +237,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
           const float o[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
           float y[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) y[i] = cb.yb[8 * r8 + i][tid];
+          for (int i = 0; i < 8; ++i) y[i] = cb.at(8 * r8 + i, tid);
 #pragma unroll
           for (int i = 0; i < 8; ++i) b1p[i & 3] = fma((double)y[i], (double)o[i], b1p[i & 3]);
         }
