@@ -459,9 +459,9 @@ __device__ __forceinline__ float other_half(float x, int half) {
 // weight) and stages half `half` of the bg row of column sl of chunk c, then of chunk c + 1;
 // the weight of the column it stages but does not own comes from lane sl + 32 (half 0) or
 // sl (half 1) by one swap.  Same columns, order and arithmetic as stage_columns.
-template <int KP, int CHUNK, int PITCH, bool SWZ, class Acc>
+template <int KP, int CHUNK, int PITCH, bool SWZ, bool XSW = false, class Acc>
 __device__ __forceinline__ int stage_columns_pair(
-    ColumnChunk<KP, CHUNK, float, PITCH, SWZ> &ch, const TreeDesc *__restrict__ trees,
+    ColumnChunk<KP, CHUNK, float, PITCH, SWZ, XSW> &ch, const TreeDesc *__restrict__ trees,
     const SolveConsts &c, int gi, int lane, const int *__restrict__ nbr_cnt,
     const int *__restrict__ nbr_idx, const float3 pt, Acc &&accumulate) {
   static_assert(CHUNK == 32, "two lanes per staged column");
@@ -471,9 +471,15 @@ __device__ __forceinline__ int stage_columns_pair(
   if (lane < 32) ch.expt[lane] = kExpT[lane];
   if constexpr (PITCH > KP + 1) {
     constexpr int NZ = PITCH - KP - 1;
-    for (int e = lane; e < CHUNK * NZ; e += 64) ch.col(e / NZ)[KP + 1 + e % NZ] = 0.0f;
+    for (int e = lane; e < CHUNK * NZ; e += 64) ch.at(e / NZ, KP + 1 + e % NZ) = 0.0f;
   }
   const int sl = lane % CHUNK, half = lane / CHUNK;
+  // XSW (pitches 32, 64): the lane gathers and stores its VH / 2 float4 starting at float4
+  // (sl >> 1) mod VH / 2, so a 16-lane store group writes several row offsets, with the odd
+  // columns' r ^ 16 on top (ColumnChunk), instead of one
+  constexpr int NQ = VH / 2;
+  const int rot = XSW ? (sl >> 1) % NQ : 0;
+  auto quad = [&](int i) { return XSW ? (i + rot >= NQ ? i + rot - NQ : i + rot) : i; };
   for (int t = 0; t < c.ntrees; ++t) {
     const TreeDesc T = trees[t];
     const float q0 = pt.x * T.hclr_inv, q1 = pt.y * T.hclr_inv;  // get_lz (:243-253)
@@ -498,14 +504,14 @@ __device__ __forceinline__ int stage_columns_pair(
     auto gather_bg = [&](int col, f32x4 (&g)[VH / 2]) {
       const unsigned b0 = (unsigned)(col * KP + 2 * VH * half);
 #pragma unroll
-      for (int i = 0; i < VH / 2; ++i) g[i] = gld4(T.col_bg, b0 + 4u * i);
+      for (int i = 0; i < VH / 2; ++i) g[i] = gld4(T.col_bg, b0 + 4u * (unsigned)quad(i));
     };
     auto put = [&](const f32x4 (&g)[VH / 2], float w) {  // bg * error_inv (:452)
-      float *d = ch.col(sl) + 2 * VH * half;
 #pragma unroll
       for (int i = 0; i < VH / 2; ++i) {
-        *reinterpret_cast<float2 *>(d + 4 * i) = make_float2(g[i].x * w, g[i].y * w);
-        *reinterpret_cast<float2 *>(d + 4 * i + 2) = make_float2(g[i].z * w, g[i].w * w);
+        const int r = 2 * VH * half + 4 * quad(i);
+        *reinterpret_cast<float2 *>(&ch.at(sl, r)) = make_float2(g[i].x * w, g[i].y * w);
+        *reinterpret_cast<float2 *>(&ch.at(sl, r + 2)) = make_float2(g[i].z * w, g[i].w * w);
       }
     };
     int slot_next = slot_at(half * CHUNK + sl);
@@ -536,7 +542,7 @@ __device__ __forceinline__ int stage_columns_pair(
       const float w_b = half ? w : w_x;
       if (half == 0) {
         ch.yo[sl] = yo;
-        if constexpr (PITCH > KP) ch.col(sl)[KP] = yo;
+        if constexpr (PITCH > KP) ch.at(sl, KP) = yo;
       }
       put(g, half ? w_x : w);
       const bool two = base + CHUNK < npairs;  // wave-uniform
@@ -547,7 +553,7 @@ __device__ __forceinline__ int stage_columns_pair(
       if (two) {
         if (half == 1) {
           ch.yo[sl] = yo;
-          if constexpr (PITCH > KP) ch.col(sl)[KP] = yo;
+          if constexpr (PITCH > KP) ch.at(sl, KP) = yo;
         }
         put(g, w_b);
         __syncthreads();
@@ -746,13 +752,15 @@ struct MfmaLayout {
   static constexpr int NTL = NT * (NT + 1) / 2;          // lower tiles
   static constexpr int PITCH = YO_ROW ? 16 * NT : KP;    // staged column length
   static constexpr bool SWZ = PITCH % 32 == 16;          // shifted columns (ColumnChunk)
+  static constexpr bool XSW = PITCH % 32 == 0;           // odd columns' rows ^ 16 (ColumnChunk)
   static constexpr int NBL4 = YO_ROW ? (KP + 1 - 16 * (NT - 1) + 3) / 4 : 4;  // live strips
   static constexpr bool SPLIT_LAST = NBL4 < 4;
 };
 
 template <int KP, int CHUNK, bool ASSEMBLED>
 __device__ __forceinline__ void assemble_point_mfma(
-    ColumnChunk<KP, CHUNK, float, MfmaLayout<KP>::PITCH, MfmaLayout<KP>::SWZ> &ch,
+    ColumnChunk<KP, CHUNK, float, MfmaLayout<KP>::PITCH, MfmaLayout<KP>::SWZ,
+                MfmaLayout<KP>::XSW> &ch,
     const TreeDesc *__restrict__ trees,
     const SolveConsts &c, int gi, int lane, const int *__restrict__ nbr_cnt,
     const int *__restrict__ nbr_idx, const float3 pt, const long long *__restrict__ col_off,
@@ -782,17 +790,18 @@ __device__ __forceinline__ void assemble_point_mfma(
         constexpr int NS = L::SPLIT_LAST ? L::NBL4 : 1;
         float f[2][L::NT], fy[2], fs[2][NS];
         const float *c0 = ch.col(kk);  // column 4 g + kk at c0 + g GSTRIDE
+        const int xk = ch.xr(kk);      // (XSW: the rows of an odd column are r ^ 16)
         auto load = [&](int b, int g) {
           const float *cs = c0 + g * ch.GSTRIDE;
 #pragma unroll
           for (int I = 0; I < L::NT; ++I) {
             const int row = 16 * I + m;
-            if constexpr (L::YO_ROW) f[b][I] = cs[row];
-            else f[b][I] = cs[row < KP ? row : KP - 1];
+            if constexpr (L::YO_ROW) f[b][I] = cs[row ^ xk];
+            else f[b][I] = cs[(row < KP ? row : KP - 1) ^ xk];
           }
           if constexpr (L::SPLIT_LAST) {  // strip rows, broadcast over the 4 blocks
 #pragma unroll
-            for (int r = 0; r < NS; ++r) fs[b][r] = cs[16 * (L::NT - 1) + 4 * r + (m & 3)];
+            for (int r = 0; r < NS; ++r) fs[b][r] = cs[(16 * (L::NT - 1) + 4 * r + (m & 3)) ^ xk];
           }
           if constexpr (!L::YO_ROW) fy[b] = ch.yo[4 * g + kk];
         };
@@ -832,7 +841,7 @@ __device__ __forceinline__ void assemble_point_mfma(
         }
         if constexpr (!L::YO_ROW) {
           for (int s = 0; s < nsl; ++s)
-            if (lane < KP) b1acc = fma((double)ch.col(s)[lane], (double)ch.yo[s], b1acc);
+            if (lane < KP) b1acc = fma((double)ch.at(s, lane), (double)ch.yo[s], b1acc);
         }
       });
 }

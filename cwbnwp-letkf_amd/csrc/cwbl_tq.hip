@@ -80,7 +80,7 @@ struct TqSmem {
   static constexpr int pb2_base(int J2) { return REG - (NB2 - J2) * PLD2; }
   union {
     ColumnChunk<KP, kTqChunk, TqStage, kTqMfmaAssembly ? MfmaLayout<KP>::PITCH : KP,
-                kTqMfmaAssembly && MfmaLayout<KP>::SWZ> ch;
+                kTqMfmaAssembly && MfmaLayout<KP>::SWZ, kTqMfmaAssembly && MfmaLayout<KP>::XSW> ch;
     double ah[KP / 2][KP + 2];            // half of A on its way from MFMA tiles to blocks
     double reg[REG];                      // hv[0, NHV) | y after the loop | pb
   } u;
