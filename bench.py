@@ -478,8 +478,8 @@ def main():
         flops = synth.flops_total(k, solved, nobs_sum)
         achieved = flops / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else 0.0
         kp = ((k + 7) // 8) * 8 if k <= 64 else (96 if k <= 96 else 128)
-        if kp == 32 and not jacobi and os.environ.get("CWBL_TQ4", "1") != "0":
-            kp = 40  # k = 25..32 run the KP = 40 record path (cwbl_init)
+        if kp in (24, 32) and not jacobi and os.environ.get("CWBL_TQ4", "1") != "0":
+            kp = 40  # k = 17..32 run the KP = 40 record path (cwbl_init)
         tq4 = os.environ.get("CWBL_TQ4", "1")
         split = not jacobi and kp == 40 and tq4 != "0"
         # the host's rule (cwbl_analyze_var): KP = 96 / 128 split after kp - 64 steps when

@@ -479,10 +479,11 @@ int cwbl_init(const cwbl_init_params *p) {
   if (const char *e = std::getenv("CWBL_TAIL_DIV")) S.tail_div = std::atoi(e);
   S.serial_search = false;
   if (const char *e = std::getenv("CWBL_DEBUG_SERIAL")) S.serial_search = std::atoi(e) != 0;
-  // k = 25..32: the KP = 40 record path (assembly + four-point solve; the padding rows are
-  // the identity and the steps past k - 2 exact no-ops) beats the one-wavefront KP = 32 solve
-  // (C2 grid: 91.6 against 134 ms per variable at k = 32)
-  if (S.kp == 32 && S.tq4 && !S.jacobi) S.kp = kTq4KP;
+  // k = 17..32: the KP = 40 record path (assembly + four-point solve; the padding rows are
+  // the identity and the steps past k - 2 exact no-ops) beats the one-wavefront KP = 24 / 32
+  // solves (C2 grid, r2: 91.6 against 134 ms per variable at k = 32; r3: ~75 against 79 / 88
+  // at k = 20 / 24); at k <= 16 the one-wavefront solve is faster (68 ms)
+  if ((S.kp == 24 || S.kp == 32) && S.tq4 && !S.jacobi) S.kp = kTq4KP;
   S.max_batch = 160000;
   S.max_batch_set = false;
   if (const char *e = std::getenv("CWBL_MAX_BATCH")) {

@@ -250,12 +250,12 @@ def test_synthetic_c2_subdomain_vs_oracle():
     assert st.nonconverged == 0
 
 
-@pytest.mark.parametrize("k", [25, 32, 33, 36, 40])
+@pytest.mark.parametrize("k", [17, 20, 24, 25, 32, 33, 36, 40])
 def test_split_kp40_path_vs_one_kernel_and_oracle(k, monkeypatch):
     """The KP = 40 slab path runs split by default (assemble_record_kernel writes A and Yb d,
     solve_tq40_kernel runs the whole tridiagonalisation four points per wavefront, CWBL_TQ4=1).
     k < 40 exercises the identity padding (the no-op steps past
-    k - 2); k = 25..32 run at KP = 40 too (their one-kernel path, CWBL_TQ4=0, is KP = 32).
+    k - 2); k = 17..32 run at KP = 40 too (their one-kernel paths, CWBL_TQ4=0, are KP = 24, 32).
     Both against the one-kernel path (CWBL_TQ4=0) and the oracle on a 30x30x50 C2-shaped
     grid."""
     import ctypes as C
