@@ -78,6 +78,20 @@ __device__ __forceinline__ double fnmac_row(double acc, double x, double y) {
 }
 __device__ __forceinline__ void dpp_pin(double &x) { asm volatile("s_nop 1" : "+v"(x)); }
 
+// Sum over this lane's 16-lane row, the same value on every lane: two quad_perm stages (two
+// v_mov_b32_dpp and a v_add_f64 each: gfx950 has no 64-bit quad_perm), then the four quad
+// sums Q0 + Q4 + Q8 + Q12 as one row_newbcast move and three fused v_fmac_f64_dpp (x 1.0,
+// one rounding each, as an add): 10 VALU instructions instead of row16_sum's 12.  The quad
+// sum is read by DPP two or more wait states after its add (the move's own hazard nop).
+__device__ __forceinline__ double rsum16(double v) {
+  v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
+  double s = rbcast<0>(v);
+  s = fmac_row<4>(s, v, 1.0);
+  s = fmac_row<8>(s, v, 1.0);
+  return fmac_row<12>(s, v, 1.0);
+}
+
 }  // namespace
 
 template <int KP>
@@ -231,9 +245,9 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       xu = fma(x[r], ux[r], xu);
       xb = fma(x[r], ub[r], xb);
     });
-    xx = row16_sum(xx);
-    xu = row16_sum(xu);
-    xb = row16_sum(xb);
+    xx = rsum16(xx);
+    xu = rsum16(xu);
+    xb = rsum16(xb);
     const Refl h = dlarfg(alpha, xx);
     // every lane of the row writes the same value (no divergent branch in the step)
     sm.tq[q][j][0] = dj;
@@ -295,7 +309,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         constexpr int r = decltype(rr)::value;
         s = fma(A[r][col], v[r], s);
       });
-      s = row16_sum(s);
+      s = rsum16(s);
       pP += l == col ? s : 0.0;
     });
     double pp[NS], sp = vP * pP;  // rows <= j: v = 0
@@ -304,7 +318,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       pp[r] = p0[r] + p1[r];
       sp = fma(v[r], pp[r], sp);
     });
-    const double s1 = tau * row16_sum(sp);  // v^T (tau A v)
+    const double s1 = tau * rsum16(sp);  // v^T (tau A v)
     const double wP = (pre && l > j) ? fma(-0.5 * tau * s1, vP, tau * pP) : 0.0;
     double wv[NS];
     sfor<NS>([&](auto rr) {
@@ -366,9 +380,9 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
           x[r] = 0.0;
         }
       });
-      xx = row16_sum(xx);
-      xu = row16_sum(xu);
-      xb = row16_sum(xb);
+      xx = rsum16(xx);
+      xu = rsum16(xu);
+      xb = rsum16(xb);
       const Refl h = dlarfg(alpha, xx);
       const double tau = h.tau;
       sm.tq[q][j][0] = dj;
@@ -410,7 +424,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         pp[r] = p0[r] + p1[r];
         if constexpr (16 * r + 15 > jl) sp = fma(v[r], pp[r], sp);  // rows <= j: v = 0
       });
-      const double s1 = tau * row16_sum(sp);  // v^T (tau A v)
+      const double s1 = tau * rsum16(sp);  // v^T (tau A v)
       double wv[NS];
       sfor<NS>([&](auto rr) {
         constexpr int r = decltype(rr)::value;
@@ -455,7 +469,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       const int i = l + 16 * r;
       if (16 * r + 15 < KP || i < KP) tp += i < k ? sm.tq[q][i < KP ? i : 0][0] : 0.0;
     });
-    trace = row16_sum(tp);
+    trace = rsum16(tp);
   }
 
   if constexpr (STOP == 2) {  // timing ablation: tridiagonalisation only
@@ -568,7 +582,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     const double u1 = vs == 0 ? ubP : ub[vs > 0 ? vs - 1 : 0];
     dpart = i < KP ? fma(u1, z[vs], dpart) : dpart;
   });
-  const double d = row16_sum(dpart);
+  const double d = rsum16(dpart);
   if constexpr (STOP == 3) {  // timing ablation: up to the quadrature
     if (valid && l == 0) info[gi] = make_int2(ptot, (int)(d + ys[0] + ys[1] + ys[2]));
     return;
@@ -591,7 +605,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         vv[r] = 0.0;
       }
     });
-    a = row16_sum(a);
+    a = rsum16(a);
     sfor<NS>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
       if constexpr (16 * r + 15 >= J1) y[r + 1] = fma(-tj * a, vv[r], y[r + 1]);
@@ -611,7 +625,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       else vv[r] = pr;
       a = fma(vv[r], y[r + 1], a);
     });
-    a = row16_sum(a);
+    a = rsum16(a);
     y[0] = fma(-tj * a, v0, y[0]);
     sfor<NS>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
