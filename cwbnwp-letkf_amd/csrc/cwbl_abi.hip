@@ -107,7 +107,6 @@ struct State {
   DevBuf wsa2, info2;                                 // second record / info buffers
   std::vector<hipEvent_t> cevents;                    // record-path events (cevent)
   int lead_div = 0;                                   // first batch = npts / lead_div (0: off)
-  int tail_div = 0;                                   // last batch split: 1/tail_div (0: off)
   bool serial_search = false;                         // CWBL_DEBUG_SERIAL=1: searches on S.stream
   // Points per search/solve batch.  Measured on C2 (one GPU, ms per variable): 40 k 113,
   // 70 k 110, 100 k 108, 150 k 107, 200 k 106, 500 k 109; and on an eighth of the grid (a
@@ -394,7 +393,6 @@ SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps,
   c.quad_r = S.quad.as<double2>();
   c.quad = c.quad_r;
   if (const char *e = std::getenv("CWBL_DEBUG_TQ_STOP")) c.debug_stop = std::atoi(e);
-  if (const char *e = std::getenv("CWBL_DEBUG_STAGGER")) c.stagger = std::atoi(e);
   if (const char *e = std::getenv("CWBL_DEBUG_TQ_STEPS")) c.debug_steps = std::atoi(e);
   return c;
 }
@@ -476,7 +474,6 @@ int cwbl_init(const cwbl_init_params *p) {
   if (const char *e = std::getenv("CWBL_BIG_SPLIT")) S.big_split = std::atoi(e) != 0;
   if (const char *e = std::getenv("CWBL_BIG_SUB")) S.big_sub = std::max(64LL, std::atoll(e));
   if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
-  if (const char *e = std::getenv("CWBL_TAIL_DIV")) S.tail_div = std::atoi(e);
   S.serial_search = false;
   if (const char *e = std::getenv("CWBL_DEBUG_SERIAL")) S.serial_search = std::atoi(e) != 0;
   // k = 17..32: the KP = 40 record path (assembly + four-point solve; the padding rows are
@@ -666,16 +663,8 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     long long Br = round_up((rest + nrest - 1) / nrest);
     for (long long g = g1; g < npts; g += Br)
       plan.push_back({g, (int)std::min<long long>(Br, npts - g)});
-    // optional short tail: the last batch's solve has nothing beside it, so split off its
-    // last 1/tail_div (CWBL_TAIL_DIV; 0: off)
-    if (S.tail_div > 1 && plan.size() >= 2) {
-      const auto last = plan.back();
-      const long long t = round_up(last.second / S.tail_div);
-      if (t >= 4 * kListLanes && t < last.second) {
-        plan.back().second = (int)(last.second - t);
-        plan.push_back({last.first + last.second - t, (int)t});
-      }
-    }
+    // (a short tail batch, the last batch's final 1/2 or 1/4 split off, measured within the
+    // run-to-run spread at the 8-rank share, r2: DESIGN.md §6)
     B = 0;
     for (const auto &b : plan) B = std::max<long long>(B, b.second);
   }

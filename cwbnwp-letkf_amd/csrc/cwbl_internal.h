@@ -89,7 +89,6 @@ struct SolveConsts {
   const double2 *quad;        // = quad_r (non-null once the tables are built)
   const double2 *quad_r;      // [4][kQuadLevels][kQuadStride] (t2, w) of the x^-1/2 rules of
                               // 8 R - 1 nodes, R = 2, 3, 4, 8 (quad_rule)
-  int   stagger;              // CWBL_DEBUG_STAGGER: start-phase offset unit in cycles (experiment)
   int   debug_stop;           // CWBL_DEBUG_TQ_STOP: 1 = after assembly, 2 = after
                               // tridiagonalisation, 3 = after quadrature, 4 = after the first
                               // kTq40J0 steps of solve_tq40_kernel (timing ablation only)

@@ -119,10 +119,6 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   if (gi >= npts) return;
   const int lane = threadIdx.x;
   const int k = c.k;
-  if (c.stagger > 0 && blockIdx.x < 4096) {  // experiment: offset the first waves' phases
-    const int slot = (int)(blockIdx.x >> 8) >> 2;  // 0..3 for the 16 first-round slots of a CU
-    for (int t = 0; t < slot * c.stagger / 8000; ++t) __builtin_amdgcn_s_sleep(125);
-  }
 
   long long P = 0;  // var index of member 0
   float3 pt = make_float3(0.0f, 0.0f, 0.0f);  // the point's projected x, y and altitude
