@@ -459,11 +459,20 @@ __device__ __forceinline__ float other_half(float x, int half) {
 // weight) and stages half `half` of the bg row of column sl of chunk c, then of chunk c + 1;
 // the weight of the column it stages but does not own comes from lane sl + 32 (half 0) or
 // sl (half 1) by one swap.  Same columns, order and arithmetic as stage_columns.
-template <int KP, int CHUNK, int PITCH, bool SWZ, bool XSW = false, class Acc>
+// `side` may stage part of each column a second time, elsewhere (the record kernel's fp64
+// rows): side.stage(half, sl, g, w) sees every lane's gathered bg quads and weight right
+// after they are staged, side.yo(sl, yo) every staged yo.
+struct NoSide {
+  template <class G>
+  __device__ __forceinline__ void stage(int, int, const G &, float) {}
+  __device__ __forceinline__ void yo(int, float) {}
+};
+template <int KP, int CHUNK, int PITCH, bool SWZ, bool XSW = false, class Acc,
+          class Side = NoSide>
 __device__ __forceinline__ int stage_columns_pair(
     ColumnChunk<KP, CHUNK, float, PITCH, SWZ, XSW> &ch, const TreeDesc *__restrict__ trees,
     const SolveConsts &c, int gi, int lane, const int *__restrict__ nbr_cnt,
-    const int *__restrict__ nbr_idx, const float3 pt, Acc &&accumulate) {
+    const int *__restrict__ nbr_idx, const float3 pt, Acc &&accumulate, Side &&side = Side{}) {
   static_assert(CHUNK == 32, "two lanes per staged column");
   constexpr int VH = KP / 4;  // float2 of the bg row per lane
   static_assert(KP % 8 == 0, "bg row split into 16-B loads");
@@ -543,8 +552,10 @@ __device__ __forceinline__ int stage_columns_pair(
       if (half == 0) {
         ch.yo[sl] = yo;
         if constexpr (PITCH > KP) ch.at(sl, KP) = yo;
+        side.yo(sl, yo);
       }
       put(g, half ? w_x : w);
+      side.stage(half, sl, g, half ? w_x : w);
       const bool two = base + CHUNK < npairs;  // wave-uniform
       if (two) gather_bg(col_b, g);  // chunk c + 1's bg rows in flight during chunk c's MFMAs
       __syncthreads();
@@ -554,8 +565,10 @@ __device__ __forceinline__ int stage_columns_pair(
         if (half == 1) {
           ch.yo[sl] = yo;
           if constexpr (PITCH > KP) ch.at(sl, KP) = yo;
+          side.yo(sl, yo);
         }
         put(g, w_b);
+        side.stage(half, sl, g, w_b);
         __syncthreads();
         accumulate(min(CHUNK, npairs - base - CHUNK));
         __syncthreads();

@@ -685,10 +685,38 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   };
   constexpr int kRowA[16] = {32, 33, 34, 35, 36, 37, 38, 39, 36, 37, 38, 39, 35, 39, 0, 16};
   constexpr int kColB[16] = {YO, 32, 33, 34, YO, 35, 36, 37, 32, 33, 34, 38, 35, 39, 0, 16};
-  const int ra = pick(kRowA, m), cb = pick(kColB, m);
+  // rows of the strips and the corner in the fp64 side rows (StripRows): 32..39 -> 0..7,
+  // yo -> 8, row 0 -> 9, row 16 -> 10
+  auto srow = [](int r) { return r == YO ? 8 : r == 0 ? 9 : r == 16 ? 10 : r - 32; };
+  const int ia = srow(pick(kRowA, m)), ib = srow(pick(kColB, m));
   // A rows of the diagonal tiles: yo in place of rows 0 and 16 (read from the staged yo row,
   // not selected after the conversion: 2 reads instead of 4 v_cndmask per group)
   const int r0 = m == 0 ? YO : m, r1 = m == 0 ? YO : 16 + m;
+  // The strip and corner operands (rows 32..39, yo, 0, 16: four of a lane's eight per group,
+  // each shared by 4 to 16 lanes) are also staged as fp64, converted once per value by the
+  // staging lane instead of once per reading lane: 4 fewer v_cvt_f64_f32 per lane and group
+  // (8 groups per chunk) for 11 per chunk at staging.  Columns 96 B apart: the 32 lanes of a
+  // half wave (columns 4 g + kk, kk in {0, 1} or {2, 3}) read 24 distinct dwords each.
+  struct StripRows {
+    double d[kTqChunk][12];
+  };
+  __shared__ StripRows sr;
+  struct Side {
+    StripRows &s;
+    __device__ __forceinline__ void stage(int half, int sl, const f32x4 (&g)[KP / 8], float w) {
+      double *d = s.d[sl];
+      if (half) {  // rows 32..39 (this lane stages rows 20..39)
+        d[0] = (double)(g[3].x * w); d[1] = (double)(g[3].y * w);
+        d[2] = (double)(g[3].z * w); d[3] = (double)(g[3].w * w);
+        d[4] = (double)(g[4].x * w); d[5] = (double)(g[4].y * w);
+        d[6] = (double)(g[4].z * w); d[7] = (double)(g[4].w * w);
+      } else {  // rows 0 and 16 (rows 0..19)
+        d[9] = (double)(g[0].x * w);
+        d[10] = (double)(g[4].x * w);
+      }
+    }
+    __device__ __forceinline__ void yo(int sl, float y) { s.d[sl][8] = (double)y; }
+  };
   f64x4 t0 = {0.0, 0.0, 0.0, 0.0}, t1 = t0, t2 = t0;
   double st[4] = {0.0, 0.0, 0.0, 0.0}, cn = 0.0;
   const int ptot = stage_columns_pair<KP, kTqChunk, PITCH>(
@@ -696,18 +724,21 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
         // column s = 4 g + kk of the chunk is k-slot kk of group g; staged columns past nsl
         // are zero.  The group loop is unrolled with a static double buffer: group g + 1's
         // operands are read before group g's MFMAs.
-        float f[2][8];
+        float f[2][4];
+        double e[2][4];
         const float *c0 = ch.col(kk);  // column 4 g + kk at c0 + g GSTRIDE
+        const double *d0 = sr.d[kk];   // its side rows at d0 + 48 g
         auto load = [&](int b, int g) {
           const float *col = c0 + g * ch.GSTRIDE;
           f[b][0] = col[m];
           f[b][1] = col[16 + m];
           f[b][2] = col[r0];
-          f[b][3] = col[32 + (m & 3)];
-          f[b][4] = col[36 + (m & 3)];
-          f[b][5] = col[ra];
-          f[b][6] = col[cb];
-          f[b][7] = col[r1];
+          f[b][3] = col[r1];
+          const double *dc = d0 + 48 * g;
+          e[b][0] = dc[m & 3];
+          e[b][1] = dc[4 + (m & 3)];
+          e[b][2] = dc[ia];
+          e[b][3] = dc[ib];
         };
         const int nl = c.debug_stop == 11 ? 0 : nsl;
         if (nl > 0) load(0, 0);
@@ -716,9 +747,9 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
           if (4 * g >= nl) break;  // nsl is wave-uniform
           const int b = g & 1;
           const double o0 = (double)f[b][0], o1 = (double)f[b][1];
-          const double a0 = (double)f[b][2], a1 = (double)f[b][7];
-          const double s0 = (double)f[b][3], s1 = (double)f[b][4];
-          const double ca = (double)f[b][5], cbv = (double)f[b][6];
+          const double a0 = (double)f[b][2], a1 = (double)f[b][3];
+          const double s0 = e[b][0], s1 = e[b][1];
+          const double ca = e[b][2], cbv = e[b][3];
           if (g + 1 < kTqChunk / 4 && 4 * (g + 1) < nl) load(b ^ 1, g + 1);
           t0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, o0, t0, 0, 0, 0);
           t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(o1, o0, t1, 0, 0, 0);
@@ -729,7 +760,8 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
           st[3] = __builtin_amdgcn_mfma_f64_4x4x4f64(s1, o1, st[3], 0, 0, 0);
           cn = __builtin_amdgcn_mfma_f64_4x4x4f64(ca, cbv, cn, 0, 0, 0);
         }
-      });
+      },
+      Side{sr});
   if (lane == 0) info[gi] = make_int2(ptot, 0);  // p = 0: the solve leaves var unchanged
   if (ptot == 0) return;
   if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the record
