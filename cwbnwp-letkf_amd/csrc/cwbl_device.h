@@ -463,6 +463,7 @@ __device__ __forceinline__ float other_half(float x, int half) {
 // rows): side.stage(half, sl, g, w) sees every lane's gathered bg quads and weight right
 // after they are staged, side.yo(sl, yo) every staged yo.
 struct NoSide {
+  static constexpr bool kPad = true;  // zero the chunk's padding rows KP + 1 .. PITCH - 1
   template <class G>
   __device__ __forceinline__ void stage(int, int, const G &, float) {}
   __device__ __forceinline__ void yo(int, float) {}
@@ -478,7 +479,7 @@ __device__ __forceinline__ int stage_columns_pair(
   static_assert(KP % 8 == 0, "bg row split into 16-B loads");
   int ptot = 0;
   if (lane < 32) ch.expt[lane] = kExpT[lane];
-  if constexpr (PITCH > KP + 1) {
+  if constexpr (PITCH > KP + 1 && std::decay_t<Side>::kPad) {
     constexpr int NZ = PITCH - KP - 1;
     for (int e = lane; e < CHUNK * NZ; e += 64) ch.at(e / NZ, KP + 1 + e % NZ) = 0.0f;
   }

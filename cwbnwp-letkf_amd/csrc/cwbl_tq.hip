@@ -661,6 +661,29 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
 // cycles of work; 1.27x), against 336 for the 48 x 48 tiling with a yo strip (1.56x).  Every
 // entry is one fp64 FMA chain over the columns in staging order, like the reference's
 // dsyrk/dgemv (products of fp32 values are exact in fp64).
+// The record kernel's fp64 side rows of a staged chunk (see assemble_record_kernel): per
+// column rows 32..39, yo, row 0, row 16 (and one pad word: columns 96 B apart)
+struct RecordStripRows {
+  double d[kTqChunk][12];
+};
+struct RecordSide {
+  static constexpr bool kPad = false;  // the chunk's rows past 31 (but yo) are never read
+  RecordStripRows &s;
+  __device__ __forceinline__ void stage(int half, int sl, const f32x4 (&g)[kTq4KP / 8], float w) {
+    double *d = s.d[sl];
+    if (half) {  // rows 32..39 (this lane stages rows 20..39)
+      d[0] = (double)(g[3].x * w); d[1] = (double)(g[3].y * w);
+      d[2] = (double)(g[3].z * w); d[3] = (double)(g[3].w * w);
+      d[4] = (double)(g[4].x * w); d[5] = (double)(g[4].y * w);
+      d[6] = (double)(g[4].z * w); d[7] = (double)(g[4].w * w);
+    } else {  // rows 0 and 16 (rows 0..19)
+      d[9] = (double)(g[0].x * w);
+      d[10] = (double)(g[4].x * w);
+    }
+  }
+  __device__ __forceinline__ void yo(int sl, float y) { s.d[sl][8] = (double)y; }
+};
+
 template <int WAVES>
 __global__ void __launch_bounds__(64, WAVES)
 assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
@@ -676,19 +699,22 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   const int lane = threadIdx.x, kk = lane >> 4, m = lane & 15;
   float3 pt;
   slab_point(slab, g0 + gi, pt.x, pt.y, pt.z);
-  // corner operands of this lane (m = 4 b + i for the A rows, 4 b + j for the B columns)
-  auto pick = [](const int (&t)[16], int i) {
-    int v = 0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) v = i == q ? t[q] : v;
-    return v;
+  // corner operands of this lane (m = 4 b + i for the A rows, 4 b + j for the B columns):
+  // entry i of a 16-entry byte table held as two 64-bit literals (a shift and a mask, not 16
+  // compares and selects per lookup)
+  struct Tab16 {
+    unsigned long long lo, hi;
+    __device__ __forceinline__ int operator[](int i) const {
+      return (int)(((i < 8 ? lo : hi) >> (8 * (i & 7))) & 0xffull);
+    }
   };
-  constexpr int kRowA[16] = {32, 33, 34, 35, 36, 37, 38, 39, 36, 37, 38, 39, 35, 39, 0, 16};
-  constexpr int kColB[16] = {YO, 32, 33, 34, YO, 35, 36, 37, 32, 33, 34, 38, 35, 39, 0, 16};
-  // rows of the strips and the corner in the fp64 side rows (StripRows): 32..39 -> 0..7,
-  // yo -> 8, row 0 -> 9, row 16 -> 10
-  auto srow = [](int r) { return r == YO ? 8 : r == 0 ? 9 : r == 16 ? 10 : r - 32; };
-  const int ia = srow(pick(kRowA, m)), ib = srow(pick(kColB, m));
+  constexpr Tab16 kRowA = {0x2726252423222120ull, 0x1000272327262524ull};  // 32..39 36..39 35 39 0 16
+  constexpr Tab16 kColB = {0x2524232822212028ull, 0x1000272326222120ull};  // yo 32..34 yo 35..37 32..34 38 35 39 0 16
+  // rows of the strips and the corner in the fp64 side rows (RecordStripRows): 32..39 ->
+  // 0..7, yo -> 8, row 0 -> 9, row 16 -> 10
+  constexpr Tab16 kRowD = {0x0706050403020100ull, 0x0a09070307060504ull};
+  constexpr Tab16 kColD = {0x0504030802010008ull, 0x0a09070306020100ull};
+  const int ia = kRowD[m], ib = kColD[m];
   // A rows of the diagonal tiles: yo in place of rows 0 and 16 (read from the staged yo row,
   // not selected after the conversion: 2 reads instead of 4 v_cndmask per group)
   const int r0 = m == 0 ? YO : m, r1 = m == 0 ? YO : 16 + m;
@@ -697,26 +723,7 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   // staging lane instead of once per reading lane: 4 fewer v_cvt_f64_f32 per lane and group
   // (8 groups per chunk) for 11 per chunk at staging.  Columns 96 B apart: the 32 lanes of a
   // half wave (columns 4 g + kk, kk in {0, 1} or {2, 3}) read 24 distinct dwords each.
-  struct StripRows {
-    double d[kTqChunk][12];
-  };
-  __shared__ StripRows sr;
-  struct Side {
-    StripRows &s;
-    __device__ __forceinline__ void stage(int half, int sl, const f32x4 (&g)[KP / 8], float w) {
-      double *d = s.d[sl];
-      if (half) {  // rows 32..39 (this lane stages rows 20..39)
-        d[0] = (double)(g[3].x * w); d[1] = (double)(g[3].y * w);
-        d[2] = (double)(g[3].z * w); d[3] = (double)(g[3].w * w);
-        d[4] = (double)(g[4].x * w); d[5] = (double)(g[4].y * w);
-        d[6] = (double)(g[4].z * w); d[7] = (double)(g[4].w * w);
-      } else {  // rows 0 and 16 (rows 0..19)
-        d[9] = (double)(g[0].x * w);
-        d[10] = (double)(g[4].x * w);
-      }
-    }
-    __device__ __forceinline__ void yo(int sl, float y) { s.d[sl][8] = (double)y; }
-  };
+  __shared__ RecordStripRows sr;
   f64x4 t0 = {0.0, 0.0, 0.0, 0.0}, t1 = t0, t2 = t0;
   double st[4] = {0.0, 0.0, 0.0, 0.0}, cn = 0.0;
   const int ptot = stage_columns_pair<KP, kTqChunk, PITCH>(
@@ -761,7 +768,7 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
           cn = __builtin_amdgcn_mfma_f64_4x4x4f64(ca, cbv, cn, 0, 0, 0);
         }
       },
-      Side{sr});
+      RecordSide{sr});
   if (lane == 0) info[gi] = make_int2(ptot, 0);  // p = 0: the solve leaves var unchanged
   if (ptot == 0) return;
   if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the record
@@ -775,6 +782,8 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   auto put = [&](int row, int col, double a) {  // packed lower; inflat on the live diagonal
     w[HO::TA + row * (row + 1) / 2 + col] = row != col ? a : row < k ? a + inflat : 1.0;
   };
+  // entries below the diagonal (T1, the strips): no diagonal select
+  auto put_low = [&](int row, int col, double a) { w[HO::TA + row * (row + 1) / 2 + col] = a; };
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = kk + 4 * r;  // A-operand row index of the tiles
@@ -785,15 +794,15 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
       if (m <= i) put(i, m, t0[r]);
       if (m <= i) put(16 + i, 16 + m, t2[r]);
     }
-    put(16 + i, m, t1[r]);
+    put_low(16 + i, m, t1[r]);
   }
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
-    for (int J = 0; J < 2; ++J) put(32 + 4 * r + kk, 16 * J + m, st[2 * J + r]);
+    for (int J = 0; J < 2; ++J) put_low(32 + 4 * r + kk, 16 * J + m, st[2 * J + r]);
   {  // corner: lane 16 i + 4 b + j = (row kRowA[4 b + i], col kColB[4 b + j])
     const int bb = (lane >> 2) & 3, i = kk, j = lane & 3;
-    const int row = pick(kRowA, 4 * bb + i), col = pick(kColB, 4 * bb + j);
+    const int row = kRowA[4 * bb + i], col = kColB[4 * bb + j];
     if (col == YO) w[HO::U1 + row] = cn;
     else if (bb == 3 ? i == j : col <= row) put(row, col, cn);
   }
