@@ -126,7 +126,7 @@ struct State {
   int tq4 = 1;  // CWBL_TQ4: KP=40 solve 0 = one kernel, else assembly record + solve_tq40
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: record batch (points)
   bool big_split = true;                              // CWBL_BIG_SPLIT=0: one-kernel KP=128 solve
-  long long big_sub = 32768;                          // CWBL_BIG_SUB: KP=128 hand-off batch
+  long long big_sub = 98304;                          // CWBL_BIG_SUB: KP=128 hand-off batch
   std::vector<hipEvent_t> events;
   hipStream_t h2d = nullptr, d2h = nullptr;           // host-memory slab copies (pipelined)
   hipStream_t caller_stream = nullptr;                // cwbl_set_stream (null: legacy stream)
@@ -466,7 +466,8 @@ int cwbl_init(const cwbl_init_params *p) {
   S.tq40_streams = true;
   if (const char *e = std::getenv("CWBL_TQ40_STREAMS")) S.tq40_streams = std::atoi(e) != 0;
   S.big_split = true;
-  S.big_sub = 32768;
+  // (C4 per variable, r3: 32 k points 2.42 s, 16 k 2.47, 64 k 2.41, 96 k 2.39, 128 k 2.39)
+  S.big_sub = 98304;
   {
     const char *e = std::getenv("CWBL_SEARCH");
     S.binned = !(e && std::strcmp(e, "tree") == 0);
@@ -752,7 +753,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     if ((S.kp == 96 || S.kp == kBigSplitKP) && S.big_split && S.k > big_split_j0(S.kp) + 2) {
       // 256-thread assembly + first kBigJ0 steps -> workspace -> one-wavefront tail, in
       // hand-off batches of Bs points (a multiple of kListLanes; BigHandoff<128, 64> is
-      // 134.7 KB per point, 4.4 GB at the default 32 768, outside workspace_bytes)
+      // 134.7 KB per point, 13 GB at the default 98 304, outside workspace_bytes)
       const long long nsub = (nb + S.big_sub - 1) / S.big_sub;
       long long Bs = (nb + nsub - 1) / nsub;
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);

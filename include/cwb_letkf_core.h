@@ -96,7 +96,8 @@ typedef struct cwbl_init_params {
   size_t workspace_bytes;  /* device workspace budget for neighbour lists (0 = 2 GiB); the
                             * solve's per-batch records come on top: 6.9 KB per point of a
                             * search batch at k = 25..40 (two buffers), 135 KB per point of a
-                            * k = 65..128 hand-off sub-batch (CWBL_BIG_SUB, 32 768 points) */
+                            * k = 65..128 hand-off sub-batch (CWBL_BIG_SUB, at most 98 304 points:
+                            * up to 13 GB) */
 } cwbl_init_params;
 
 /* One GTS platform: type(gts_structure), module_gts_omboma.f90:13-22. */
