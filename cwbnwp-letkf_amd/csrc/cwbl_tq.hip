@@ -782,24 +782,34 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   auto put = [&](int row, int col, double a) {  // packed lower; inflat on the live diagonal
     w[HO::TA + row * (row + 1) / 2 + col] = row != col ? a : row < k ? a + inflat : 1.0;
   };
-  // entries below the diagonal (T1, the strips): no diagonal select
-  auto put_low = [&](int row, int col, double a) { w[HO::TA + row * (row + 1) / 2 + col] = a; };
+  // The tiles' and strips' entries: A(kk + c, m + d) for a compile-time (c, d) is record word
+  // TA + tri(kk + c) + m + d = TA + tri(kk) + m + c kk + tri(c) + d, i.e. one lane base, one
+  // v_mad_u32_u24 (c kk) and an immediate.  On the diagonal (m == kk + c, c < 32) the value
+  // is a + inflat on live rows and 1 on padding rows, whose a is +0: a + dd with dd = inflat
+  // or 1, and a + 0 elsewhere (a is never -0: the sums start from +0), so no store selects.
+  char *const wb = reinterpret_cast<char *>(w);
+  const unsigned b8 = 8u * (unsigned)(HO::TA + ((kk * (kk + 1)) >> 1) + m);
+  auto at = [&](int cc, int d) -> double & {
+    return *reinterpret_cast<double *>(wb + (b8 + 8u * (unsigned)cc * (unsigned)kk) +
+                                       8u * (unsigned)((cc * (cc + 1)) / 2 + d));
+  };
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = kk + 4 * r;  // A-operand row index of the tiles
-    if (i == 0) {
+    if (r == 0 && kk == 0) {
       w[HO::U1 + m] = t0[r];        // yo . Yb(m)
       w[HO::U1 + 16 + m] = t2[r];   // yo . Yb(16 + m)
-    } else {
-      if (m <= i) put(i, m, t0[r]);
-      if (m <= i) put(16 + i, 16 + m, t2[r]);
+    } else if (m <= i) {
+      const bool dg = m == i;
+      at(4 * r, 0) = t0[r] + (dg ? inflat : 0.0);                           // rows 1..15 < k
+      at(16 + 4 * r, 16) = t2[r] + (dg ? (16 + i < k ? inflat : 1.0) : 0.0);
     }
-    put_low(16 + i, m, t1[r]);
+    at(16 + 4 * r, 0) = t1[r];
   }
 #pragma unroll
   for (int r = 0; r < 2; ++r)
 #pragma unroll
-    for (int J = 0; J < 2; ++J) put_low(32 + 4 * r + kk, 16 * J + m, st[2 * J + r]);
+    for (int J = 0; J < 2; ++J) at(32 + 4 * r, 16 * J) = st[2 * J + r];
   {  // corner: lane 16 i + 4 b + j = (row kRowA[4 b + i], col kColB[4 b + j])
     const int bb = (lane >> 2) & 3, i = kk, j = lane & 3;
     const int row = kRowA[4 * bb + i], col = kColB[4 * bb + j];
