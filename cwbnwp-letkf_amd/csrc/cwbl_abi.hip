@@ -583,6 +583,8 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   cwbl_stats st;
   std::memset(&st, 0, sizeof st);
   const long long npts = (long long)sl->ix_lim * sl->iy_lim * sl->nz;
+  if (npts >= (1LL << 32))  // the kernels enumerate a slab's points in 32 bits
+    return fail(CWBL_ERR_ARG, "slab of %lld points: at most 2^32 - 1 per call", npts);
   st.points = npts;
 
   hipEvent_t e0, e1;

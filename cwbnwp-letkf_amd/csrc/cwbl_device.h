@@ -220,12 +220,11 @@ __device__ __forceinline__ f32x4 gld4(const float *base, unsigned i) {  // 16 B 
 
 // Grid point g of a slab (the enumeration g = i + ix_lim*(j + iy_lim*kz) of the reference's
 // point loop, module_letkf_core.f90:209-213): projected x, y and altitude.
+// (g < 2^32: cwbl_analyze_var rejects larger slabs, so the divisions are 32-bit)
 __device__ __forceinline__ void slab_point(const SlabDev &s, long long g, float &x, float &y,
                                            float &z) {
-  const int i = (int)(g % s.ix_lim);
-  const long long r = g / s.ix_lim;
-  const int j = (int)(r % s.iy_lim);
-  const int kz = (int)(r / s.iy_lim);
+  const unsigned gg = (unsigned)g, ix = (unsigned)s.ix_lim, iy = (unsigned)s.iy_lim;
+  const unsigned r = gg / ix, i = gg - r * ix, kz = r / iy, j = r - kz * iy;
   x = gptr(s.x)[i + (long long)s.nx * j];
   y = gptr(s.y)[i + (long long)s.nx * j];
   z = gptr(s.alt)[i + (long long)s.alt_nx * (j + (long long)s.alt_ny * kz)];

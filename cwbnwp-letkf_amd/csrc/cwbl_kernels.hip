@@ -221,11 +221,9 @@ struct SlabQuery {
     return li < npts;
   }
   __device__ void at(int gi, float &x, float &y, float &z) const {
-    const long long g = g0 + gi;
-    const int i = (int)(g % s.ix_lim);
-    const long long r = g / s.ix_lim;
-    const int j = (int)(r % s.iy_lim);
-    const int kz = (int)(r / s.iy_lim);
+    // (g < 2^32, as slab_point)
+    const unsigned g = (unsigned)(g0 + gi), ix = (unsigned)s.ix_lim, iy = (unsigned)s.iy_lim;
+    const unsigned r = g / ix, i = g - r * ix, kz = r / iy, j = r - kz * iy;
     x = s.x[i + (long long)s.nx * j];
     y = s.y[i + (long long)s.nx * j];
     z = s.alt[i + (long long)s.alt_nx * (j + (long long)s.alt_ny * kz)];
