@@ -500,10 +500,10 @@ def main():
                     args.config == pm.get("config", "c2"):
                 traffic = pm.get("hbm_bytes_per_launch")
         # executed FP64 flops per solved point of the same kernels (PMC: FP64 VALU
-        # instructions and F64 MFMA ops, profiles/r3f_fp64_flops.json): the rate the FP64
+        # instructions and F64 MFMA ops, profiles/r3g_fp64_flops.json): the rate the FP64
         # datapath actually sustains, next to the reference-algorithm-equivalent `achieved`
         executed = None
-        fl = os.path.join(REPO, "profiles", "r3f_fp64_flops.json")
+        fl = os.path.join(REPO, "profiles", "r3g_fp64_flops.json")
         if split and args.config == "c2" and os.path.exists(fl):
             with open(fl) as f:
                 fk = json.load(f)["kernels"]
