@@ -40,12 +40,48 @@ METRIC = "analysis grid-points/sec (+ wall-clock per cycle) at k=40, 1/2/4/8 MI3
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector = matrix on gfx950), spec
 
 
-def cpu_baseline(w, target_s=12.0):
+def host_cores():
+    """(logical CPUs this process may run on, physical cores among them, cgroup CPU quota or
+    None).  The reference runs flat MPI, one single-threaded rank per core
+    (cwb_letkf.f90:28): the CPU baselines use one process/thread per physical core of the
+    affinity set, capped by the cgroup's CPU quota when one is set (processes beyond the
+    quota would only be time-sliced)."""
+    aff = sorted(os.sched_getaffinity(0))
+    phys = set()
+    for c in aff:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            phys.add((open(base + "physical_package_id").read().strip(),
+                      open(base + "core_id").read().strip()))
+        except OSError:
+            phys.add(("?", str(c)))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return len(aff), len(phys), quota
+
+
+def baseline_procs():
+    n_aff, n_phys, quota = host_cores()
+    procs = n_phys if quota is None else max(1, min(n_phys, int(quota)))
+    note = (f"affinity {n_aff} logical CPUs, {n_phys} physical cores"
+            + (f", cgroup quota {quota:g} CPUs" if quota is not None else ", no cgroup quota")
+            + f"; {procs} used ({cpu_model()})")
+    return procs, note
+
+
+def cpu_baseline(w, target_s=12.0, threads=None):
     """Oracle (C restatement, OpenMP over host cores) on a bounded sample of the same
     workload: a block of whole columns cut out of the grid.  Rank 0, N=1 only."""
     from helpers import oracle
     lib = oracle()
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    note = ""
+    if threads is None:
+        threads, note = baseline_procs()
     ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
 
     def run(nb):
@@ -72,7 +108,8 @@ def cpu_baseline(w, target_s=12.0):
     return {"value": pts / dt, "unit": "grid-points/s", "cores": threads, "kind": "port",
             "sample": f"{nb}x{nb} columns x {w.nz} levels = {pts} points of the {w.name} grid "
                       f"({dt:.1f} s), mean p={st.nobs_sum / max(st.solved, 1):.0f}, "
-                      f"LAPACK={lib.orc_lapack_name().decode()}"}
+                      f"LAPACK={lib.orc_lapack_name().decode()}, {threads} OpenMP threads; "
+                      f"{note}"}
 
 
 REF_HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
@@ -97,7 +134,7 @@ def _ref_driver_blob(w, i0, j0, nb):
         f4(w.obs_xyz), f4(w.obs), f4(w.hdxb)])
 
 
-def cpu_baseline_reference(w, target_s=12.0):
+def cpu_baseline_reference(w, target_s=12.0, procs=None):
     """The reference's own compiled code (oracle/_ref/ref_harness: letkf_solve, kdtree2 and
     read_namelist built from /root/reference with amdflang + MKL dsyevd, the driver-loop glue
     restated line for line) timed on the host cores as the reference runs: flat, one
@@ -107,7 +144,9 @@ def cpu_baseline_reference(w, target_s=12.0):
     import tempfile
     if not os.path.exists(REF_HARNESS):
         return None
-    procs = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    note = ""
+    if procs is None:
+        procs, note = baseline_procs()
     env = dict(os.environ, MKL_CBWR="COMPATIBLE", MKL_THREADING_LAYER="SEQUENTIAL",
                MKL_NUM_THREADS="1", OMP_NUM_THREADS="1")
 
@@ -146,7 +185,7 @@ def cpu_baseline_reference(w, target_s=12.0):
             "sample": f"{procs} single-threaded processes (the reference's flat MPI layout), "
                       f"each {nb}x{nb} columns x {w.nz} levels of the {w.name} grid: {pts} points "
                       f"in {dt:.1f} s; reference letkf_solve/kdtree2/read_namelist compiled with "
-                      f"amdflang, MKL dsyevd (oracle/_ref/ref_harness driver)"}
+                      f"amdflang, MKL dsyevd (oracle/_ref/ref_harness driver); {note}"}
 
 
 def time_transposes(core, w, k, rank, world, dev):
@@ -190,59 +229,99 @@ CYCLE = (("U", 1.6, "u"), ("V", 1.6, "v"), ("W", 1.6, "w"), ("T", 1.6, "m"),
          ("QHAIL", 1.1, "q"), ("QNRAIN", 1.1, "q"), ("QNSNOW", 1.1, "q"),
          ("QNGRAUPEL", 1.1, "q"), ("QNHAIL", 1.1, "q"), ("MU", 1.1, "mu"), ("P", 1.1, "m"),
          ("PH", 1.1, "w"))
+# (transpose stagger, levels above nz) of each slab kind (module_letkf_core.f90:70-81)
+KINDS = {"u": (1, 0), "v": (2, 0), "w": (0, 1), "m": (0, 0), "q": (0, 0), "mu": (0, None)}
 
 
-def time_cycle(core, w, world, dev, x, y, alt):
-    """Wall-clock of one analysis cycle on this rank's columns: every var_update entry of
-    input.nml analysed with the configuration's obs set and localisation (one obs type, so
-    the k-d trees are built once and shared, as the tree cache does for variables of equal
-    localisation).  Slabs are made on the device before the timed region (synthetic
-    N(0,1) members: the cost does not depend on the values); max over ranks."""
-    cfg, k, nz = w.extra["cfg"], w.k, w.nz
+def _kind_slab(kind, x, y, alt, lx, ly):
+    """(x, y, alt) of a variable's slab on this rank's columns: U/V take one more staggered
+    column/row where the rank holds one (loc_nx_u / loc_ny_v), with mass-point altitude (Q2);
+    W/PH one level above the top; MU the lowest level."""
     ny, nx = x.shape
-    top = alt[-1:] + 400.0                      # one staggered level above the top
-    runs = []
+    xs, ys, al = x, y, alt
+    if kind == "u" and lx > nx:
+        xs = torch.cat([x, x[:, -1:] + 2e3], 1).contiguous()
+        ys = torch.cat([y, y[:, -1:]], 1).contiguous()
+    elif kind == "v" and ly > ny:
+        xs = torch.cat([x, x[-1:]], 0).contiguous()
+        ys = torch.cat([y, y[-1:] + 2e3], 0).contiguous()
+    elif kind == "w":
+        al = torch.cat([alt, alt[-1:] + 400.0], 0).contiguous()
+    elif kind == "mu":
+        al = alt[:1].contiguous()
+    return xs, ys, al
+
+
+def time_cycle(core, w, rank, world, dev, x, y, alt, transposes=True):
+    """Wall-clock of one analysis cycle on this rank: every var_update entry
+    of input.nml, each as letkf_driver runs it (module_letkf_core.f90:59-297) —
+    letkf_scatter_grid (member -> column transpose, module_mpi_util.f90:262), the analysis of
+    this rank's columns, letkf_gather_grid (column -> member, :325) — and then write_mean's
+    ensemble mean of the analysed fields (module_grid.f90:700-840, one RCCL reduce).  The
+    members are dealt m % world (k/world per rank on an 8-GPU node); the transposes are the
+    HIP packing kernels + RCCL point-to-point (cwbl/transpose.py).  One obs type, so the k-d
+    trees are built once and shared (the tree cache, as for variables of equal localisation).
+    Member fields are synthetic N(0,1) in HBM before the timed region (the cost does not
+    depend on the values).  No file I/O.  Max over ranks."""
+    from cwbl import transpose as tr
+    cfg, k, nz = w.extra["cfg"], w.k, w.nz
+    nxg, nyg = cfg["nx"], cfg["ny"]
+    t = tr.Transposer(core, k, nxg, nyg, device=dev)
+    lx0, ly0 = t.local_shape(0)
+    assert (ly0, lx0) == tuple(x.shape), ((ly0, lx0), tuple(x.shape))
+    fields, slabs, runs = {}, {}, []
+    for kind, (stg, up) in KINDS.items():
+        nzv = 1 if up is None else nz + up
+        gx, gy = t.dec.grid(stg)
+        if transposes:
+            fields[kind] = {m: torch.randn((nzv, gy, gx), device=dev) for m in t.owned()}
+        lx, ly = t.local_shape(stg)
+        slabs[kind] = (nzv, stg, lx, ly, _kind_slab(kind, x, y, alt, lx, ly),
+                       None if transposes else torch.randn((k, nzv, ly, lx), device=dev))
     for name, infl, kind in CYCLE:
-        xs, ys, al, nzv, nxv, nyv = x, y, alt, nz, nx, ny
-        if kind == "u":
-            nxv = nx + 1
-            xs = torch.cat([x, x[:, -1:] + 2e3], 1).contiguous()
-            ys = torch.cat([y, y[:, -1:]], 1).contiguous()
-        elif kind == "v":
-            nyv = ny + 1
-            xs = torch.cat([x, x[-1:]], 0).contiguous()
-            ys = torch.cat([y, y[-1:] + 2e3], 0).contiguous()
-        elif kind == "w":
-            nzv = nz + 1
-            al = torch.cat([alt, top], 0).contiguous()
-        elif kind == "mu":
-            nzv = 1
-            al = alt[:1].contiguous()
-        var = torch.randn((k, nzv, nyv, nxv), device=dev)
         vp = synth.radar_var_params(cfg["hclr"], cfg["vclr"], cfg["max_lz"], cfg["err"],
                                     cfg["err_rej"], cfg["radar_type"], multi_infl=infl)
         vp.tune_q = 1 if kind == "q" else 0
-        runs.append((name, vp, abi.make_slab(xs, ys, al, var, memory=abi.MEM_DEVICE,
-                                             ix_lim=nx, iy_lim=ny), var))
+        runs.append((name, kind, vp))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    per = {}
+    per, ms_sc, ms_an, ms_ga = {}, 0.0, 0.0, 0.0
     t0 = time.perf_counter()
-    for name, vp, slab, _ in runs:
+    for name, kind, vp in runs:
+        nzv, stg, lx, ly, (xs, ys, al), var = slabs[kind]
         ta = time.perf_counter()
-        core.analyze_var(vp, slab)
-        per[name] = round((time.perf_counter() - ta) * 1e3, 2)
+        if transposes:
+            var = t.scatter_grid(fields[kind], nzv, stg)
+        tb = time.perf_counter()
+        core.analyze_var(vp, abi.make_slab(xs, ys, al, var, memory=abi.MEM_DEVICE,
+                                           ix_lim=lx0, iy_lim=ly0))
+        tc = time.perf_counter()
+        if transposes:
+            t.gather_grid(var, stg, out=fields[kind])
+            torch.cuda.synchronize()
+        td = time.perf_counter()
+        ms_sc += (tb - ta) * 1e3
+        ms_an += (tc - tb) * 1e3
+        ms_ga += (td - tc) * 1e3
+        per[name] = round((td - ta) * 1e3, 2)
+    tm = time.perf_counter()
+    if transposes:  # write_mean: every analysed field of the owned members, one reduce
+        t.write_mean({m: [fields[kind][m] for _, _, kind in runs] for m in t.owned()})
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 1e3
-    if world > 1:
-        t = torch.tensor([ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms = float(t.item())
-    return {"cycle_ms": ms, "variables": len(CYCLE), "per_variable_ms_rank0": per,
-            "note": "input.nml var_update on this configuration's grid and obs set; "
-                    "U/V staggered (Q2), W/PH nz+1 levels, MU 1 level, tune_q on the Q "
-                    "species; analysis only (no member<->column transposes, no file I/O)"}
+    t1 = time.perf_counter()
+    vals = _max_over_ranks([(t1 - t0) * 1e3, ms_sc, ms_an, ms_ga, (t1 - tm) * 1e3], world, dev)
+    return {"cycle_ms": vals[0], "variables": len(CYCLE),
+            "scatter_ms": vals[1], "analysis_ms": vals[2], "gather_ms": vals[3],
+            "write_mean_ms": vals[4], "transposes": transposes,
+            "per_variable_ms_rank0": per,
+            "note": "input.nml var_update on this configuration's grid and obs set, per "
+                    "variable letkf_scatter_grid (HIP pack + RCCL point-to-point) -> "
+                    "cwbl_analyze_var -> letkf_gather_grid, then write_mean (member sums + "
+                    "one reduce); U/V staggered (Q2), W/PH nz+1 levels, MU 1 level, tune_q on "
+                    "the Q species; no file I/O; component times are max over ranks"
+                    if transposes else
+                    "analysis only (--no-transposes): no member<->column transposes"}
 
 
 def cpu_model():
@@ -282,6 +361,7 @@ def time_config(name, rank, world, local, dev, steps, warmup):
     slab = abi.make_slab(x, y, alt, var, memory=abi.MEM_DEVICE)
     for _ in range(warmup):
         core.analyze_var(w.vp, slab)
+    core.set_kernel_timing(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -291,24 +371,24 @@ def time_config(name, rank, world, local, dev, steps, warmup):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    ktimes = core.kernel_times()
     solved = sum(s.solved for s in stats)
     nobs = sum(s.nobs_sum for s in stats)
     ms_solve = sum(s.ms_solve for s in stats)
-    flops = synth.flops_total(w.k, solved, nobs)
+    roof, per_kernel = roofline_block(ktimes, w.k, solved, nobs, ms_solve, name)
     el, pts, sol, nsum = _max_over_ranks([el], world, dev) + _max_over_ranks(
         [float(sum(s.points for s in stats)), float(solved), float(nobs)], world, dev,
         dist.ReduceOp.SUM if world > 1 else None)
     core.finalize()
     cfg = w.extra["cfg"]
-    tf = flops / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else 0.0
     return {"workload": f"{name}: {cfg['nx']}x{cfg['ny']}x{cfg['nz']} grid, k={w.k}, "
                         f"{cfg['n_obs']} obs (hclr {cfg['hclr']} km, vclr {cfg['vclr']} km), "
                         f"max_lz_pts {cfg['max_lz']}",
             "value": pts / el, "unit": "grid-points/s", "ms_per_step": el / steps * 1e3,
-            "steps": steps, "warmup": warmup, "n_gpus": world,
+            "steps": steps, "warmup": warmup, "ranks": world,
             "mean_p": nsum / max(sol, 1),
             "nonconverged": sum(s.nonconverged for s in stats),
-            "rank0_solve_tflops_F": tf, "rank0_frac_F": tf / FP64_PEAK_TFLOPS}
+            "roofline_rank0": roof, "kernels_rank0": per_kernel}
 
 
 def time_host_memory(w, local, steps, warmup, pinned):
@@ -358,6 +438,122 @@ def self_launch(n):
     return subprocess.call(cmd)
 
 
+# ---- roofline accounting -----------------------------------------------------------------------
+# Algorithmic FP64 flops of each solve kernel: the terms of SURVEY.md §8(d)'s F(k,p) that the
+# kernel's part of the algorithm must execute, per solved point with p accepted obs:
+#   syrk + Yb d        p k(k+1) + 2pk     (module_letkf_core.f90:649, 651)
+#   tridiagonalisation sum over steps j of 4 n_j^2, n_j = k-1-j  (dsytd2: 4k^3/3 in all)
+#   reflectors on b1, x' and back      3 x 2k^2
+# (the eigendecomposition F prices at 13k^3 is never formed: the kernels apply A^-1 and
+# A^-1/2 to two vectors through T = Q^T A Q and a quadrature)
+def _tri_flops(k, j0, j1):
+    return sum(4 * (k - 1 - j) ** 2 for j in range(j0, min(j1, k - 1)))
+
+
+def kernel_algorithmic_flops(name, k, solved, nobs_sum):
+    syrk = nobs_sum * (k * (k + 1) + 2 * k)
+    vec = solved * 6 * k * k
+    if name.startswith("assemble_record_kernel"):
+        return syrk
+    if name.startswith("solve_tq40_kernel"):
+        return solved * _tri_flops(k, 0, k) + vec
+    if name.startswith("solve_tq_big_kernel") and name.count(",") == 2:  # hand-off kernel
+        j0 = int(name.split(",")[2].strip(" >"))
+        return syrk + solved * _tri_flops(k, 0, j0)
+    if name.startswith("solve_tqb_tail_kernel"):
+        j0 = int(name.split(",")[1].strip(" >"))
+        return solved * _tri_flops(k, j0, k) + vec
+    if name.startswith("solve_tq_kernel") or name.startswith("solve_tq_big_kernel"):
+        return syrk + solved * _tri_flops(k, 0, k) + vec
+    if name.startswith("solve_kernel"):  # Jacobi: the eigendecomposition itself
+        return synth.flops_total(k, solved, nobs_sum)
+    return None
+
+
+def load_pmc(config):
+    """Committed per-kernel PMC figures of `config` (profiles/pmc_kernels.json, written by
+    scripts/pmc_kernels.py from rocprofv3 passes): HBM bytes and executed FP64 flops per
+    launch, points per launch."""
+    path = os.path.join(REPO, "profiles", "pmc_kernels.json")
+    if not os.path.exists(path):
+        return {}, None
+    with open(path) as f:
+        pm = json.load(f)
+    return pm.get("configs", {}).get(config, {}), pm.get("tag")
+
+
+def roofline_block(ktimes, k, solved, nobs_sum, ms_solve, config):
+    """`roofline` of the dominant kernel (largest summed HIP-event time over the timed steps):
+    its algorithmic FP64 flops / its summed launch time; plus the solve kernels together
+    (algorithmic over the solve span), the reference-equivalent F rate and the PMC-executed
+    rates as detail."""
+    pmc, tag = load_pmc(config)
+    per = {}
+    for name, t in ktimes.items():
+        alg = kernel_algorithmic_flops(name, k, solved, nobs_sum)
+        e = {"launches": t["launches"], "points": t["points"], "ms": t["ms"],
+             "avg_launch_ms": t["ms"] / max(t["launches"], 1)}
+        if alg is not None and t["ms"] > 0:
+            e["algorithmic_tflops"] = alg / (t["ms"] * 1e-3) / 1e12
+            e["algorithmic_frac"] = e["algorithmic_tflops"] / FP64_PEAK_TFLOPS
+        pk = pmc.get(name)
+        if pk and t["ms"] > 0 and pk.get("fp64_flops_per_point"):
+            ex = pk["fp64_flops_per_point"] * t["points"] / (t["ms"] * 1e-3) / 1e12
+            e["executed_tflops"] = ex
+            e["executed_frac"] = ex / FP64_PEAK_TFLOPS
+        per[name] = e
+    solve = {n: e for n, e in per.items() if "algorithmic_tflops" in e}
+    if not solve:
+        return None, per
+    dom = max(solve, key=lambda n: solve[n]["ms"])
+    d = solve[dom]
+    alg_all = sum(kernel_algorithmic_flops(n, k, solved, nobs_sum) for n in solve)
+    F = synth.flops_total(k, solved, nobs_sum)
+    pk = pmc.get(dom, {})
+    roof = {
+        "bound": "mfma",
+        "achieved": d["algorithmic_tflops"],
+        "peak": FP64_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": d["algorithmic_frac"],
+        "traffic": pk.get("hbm_bytes_per_launch"),
+        "kernel": dom,
+        "launches": d["launches"],
+        "avg_launch_ms": d["avg_launch_ms"],
+        "note": "dominant kernel (largest summed HIP-event time, events on its own stream): "
+                "algorithmic FP64 flops of its part of letkf_solve (SURVEY.md 8(d) terms: "
+                "syrk + Yb d for the assembly; 4k^3/3 tridiagonalisation + 6k^2 for the "
+                "reflector solve) / its summed launch time; traffic = PMC HBM bytes per launch "
+                f"(profiles/pmc_kernels.json, {tag})",
+        "solve_kernels": {
+            "kernels": sorted(solve),
+            "algorithmic_tflops": alg_all / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else None,
+            "note": "all solve kernels' algorithmic flops / the solve span (ms_solve)"},
+        "reference_equivalent_F": {
+            "tflops": F / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else None,
+            "note": "F(k,p) of SURVEY.md 8(d) (13k^3 for dsyevd + the two k^3 products, never "
+                    "executed here) / the solve span: not a hardware rate"},
+    }
+    ex = [(n, e) for n, e in solve.items() if "executed_tflops" in e]
+    if len(ex) == len(solve) and ms_solve > 0:
+        tot = sum(pmc[n]["fp64_flops_per_point"] * per[n]["points"] for n in solve)
+        roof["executed"] = {"tflops": tot / (ms_solve * 1e-3) / 1e12,
+                            "frac": tot / (ms_solve * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                            "note": f"PMC-counted FP64 work ({tag}) of the solve kernels per "
+                                    "point x points / the solve span"}
+    return roof, per
+
+
+def distinct_devices(world, dev):
+    """GPUs the ranks run on (under gloo several ranks may share one)."""
+    if world == 1:
+        return 1
+    t = torch.tensor([dev.index], dtype=torch.int64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return len({int(v.item()) for v in out})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -365,8 +561,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--transposes", action="store_true",
-                    help="also time one member<->column transpose of the variable (detail only)")
+    ap.add_argument("--no-transposes", action="store_true",
+                    help="cycle without the member<->column transposes and write_mean")
     ap.add_argument("--no-cycle", action="store_true",
                     help="skip the wall-clock-per-cycle detail (16 var_update entries)")
     ap.add_argument("--no-detail-configs", action="store_true",
@@ -401,6 +597,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    n_dev = distinct_devices(world, dev)
 
     w = synth.make(args.config, shard=(rank, world) if world > 1 else None)
     k = w.k
@@ -428,6 +625,7 @@ def main():
 
     for _ in range(args.warmup):
         core.analyze_var(w.vp, slab)
+    core.set_kernel_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -439,6 +637,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ktimes = core.kernel_times()
+    core.set_kernel_timing(False)
 
     pts_local = sum(s.points for s in stats)
     if world > 1:
@@ -450,8 +650,19 @@ def main():
     else:
         pts_total = float(pts_local)
 
-    tr_detail = time_transposes(core, w, k, rank, world, dev) if args.transposes else None
-    cycle = None if args.no_cycle else time_cycle(core, w, world, dev, x, y, alt)
+    def guarded(fn, *a, **kw):
+        # a detail leg that fails is reported in `detail`, never at the cost of the JSON line
+        try:
+            return fn(*a, **kw)
+        except Exception as e:  # noqa: BLE001
+            print(f"bench.py rank {rank}: {fn.__name__} failed: {e!r}", file=sys.stderr,
+                  flush=True)
+            return {"error": repr(e)}
+
+    tr_detail = None if args.no_transposes else guarded(time_transposes, core, w, k, rank,
+                                                        world, dev)
+    cycle = None if args.no_cycle else guarded(time_cycle, core, w, rank, world, dev, x, y, alt,
+                                               transposes=not args.no_transposes)
     legs = {}
     if not args.no_detail_configs and args.config == "c2":
         # the other configurations on the same clock (detail; the library is re-initialised
@@ -459,14 +670,14 @@ def main():
         del slab, var
         core.finalize()
         torch.cuda.empty_cache()
-        legs["c4"] = time_config("c4", rank, world, local, dev, steps=2, warmup=1)
+        legs["c4"] = guarded(time_config, "c4", rank, world, local, dev, steps=2, warmup=1)
         torch.cuda.empty_cache()
-        legs["c5"] = time_config("c5", rank, world, local, dev, steps=2, warmup=1)
+        legs["c5"] = guarded(time_config, "c5", rank, world, local, dev, steps=2, warmup=1)
         torch.cuda.empty_cache()
         if world == 1:
             legs["host_memory"] = {
-                "pageable": time_host_memory(w, local, steps=3, warmup=1, pinned=False),
-                "pinned": time_host_memory(w, local, steps=3, warmup=1, pinned=True)}
+                "pageable": guarded(time_host_memory, w, local, steps=3, warmup=1, pinned=False),
+                "pinned": guarded(time_host_memory, w, local, steps=3, warmup=1, pinned=True)}
         core = abi.Core(k, device=local)  # (finalised below)
 
     if rank == 0:
@@ -475,52 +686,12 @@ def main():
         nobs_sum = sum(s.nobs_sum for s in stats)
         ms_solve = sum(s.ms_solve for s in stats)
         ms_search = sum(s.ms_search for s in stats)
-        flops = synth.flops_total(k, solved, nobs_sum)
-        achieved = flops / (ms_solve * 1e-3) / 1e12 if ms_solve > 0 else 0.0
-        kp = ((k + 7) // 8) * 8 if k <= 64 else (96 if k <= 96 else 128)
-        if kp in (24, 32) and not jacobi and os.environ.get("CWBL_TQ4", "1") != "0":
-            kp = 40  # k = 17..32 run the KP = 40 record path (cwbl_init)
-        tq4 = os.environ.get("CWBL_TQ4", "1")
-        split = not jacobi and kp == 40 and tq4 != "0"
-        # the host's rule (cwbl_analyze_var): KP = 96 / 128 split after kp - 64 steps when
-        # k > kp - 62, unless CWBL_BIG_SPLIT=0
-        split_big = kp in (96, 128) and k > kp - 62 and os.environ.get("CWBL_BIG_SPLIT", "1") != "0"
-        kpair = ("assemble_record_kernel<4>", "solve_tq40_kernel<40, 0>")
-        kname = (" + ".join(kpair) if split else
-                 f"solve_tq_big_kernel<{kp}, false, {kp - 64}> + "
-                 f"solve_tqb_tail_kernel<{kp}, {kp - 64}, 2>" if split_big else
-                 ("solve_kernel" if jacobi else
-                  "solve_tq_kernel" if kp <= 64 else "solve_tq_big_kernel") + f"<{kp}, false>")
-        traffic = None  # HBM bytes per launch from the committed PMC pass of this kernel
-        pmc = os.path.join(REPO, "profiles", "pmc_solve_traffic.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                pm = json.load(f)
-            if pm.get("kernel", "").replace("void ", "").replace("cwbl::", "") == kname and \
-                    args.config == pm.get("config", "c2"):
-                traffic = pm.get("hbm_bytes_per_launch")
-        # executed FP64 flops per solved point of the same kernels (PMC: FP64 VALU
-        # instructions and F64 MFMA ops, profiles/r3g_fp64_flops.json): the rate the FP64
-        # datapath actually sustains, next to the reference-algorithm-equivalent `achieved`
-        executed = None
-        fl = os.path.join(REPO, "profiles", "r3g_fp64_flops.json")
-        if split and args.config == "c2" and os.path.exists(fl):
-            with open(fl) as f:
-                fk = json.load(f)["kernels"]
-            ka, kb = ("cwbl::" + kn for kn in kpair)
-            if ka in fk and kb in fk and ms_solve > 0:
-                per_pt = (fk[ka]["fp64_flops_per_launch"] + fk[kb]["fp64_flops_per_launch"]) / \
-                    fk[ka]["counters_per_launch"]["SQ_WAVES"]
-                tf = per_pt * solved / (ms_solve * 1e-3) / 1e12
-                executed = {"achieved": tf, "frac": tf / FP64_PEAK_TFLOPS,
-                            "flops_per_point": per_pt,
-                            "note": "PMC-counted FP64 work (VALU full-wave + MFMA ops) per solved "
-                                    "point x points / the same solve time"}
+        roof, per_kernel = roofline_block(ktimes, k, solved, nobs_sum, ms_solve, args.config)
         out = {
             "metric": METRIC,
             "value": pts_total / elapsed,
             "unit": "grid-points/s",
-            "n_gpus": world,
+            "n_gpus": n_dev,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -537,29 +708,17 @@ def main():
                 "k": k,
                 "n_obs": n,
                 "mean_p": nobs_sum / max(solved, 1),
+                "ranks": world,
                 "parallelism": f"column-sharded x{world} (px x py = "
                                f"{'x'.join(map(str, tr_dims(world)))})" + (
                     ", obs-set broadcast over " + ("RCCL" if dist.get_backend() == "nccl"
                                                   else dist.get_backend())
                     if world > 1 else ""),
             },
-            "roofline": {
-                "bound": "mfma",
-                "achieved": achieved,
-                "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved / FP64_PEAK_TFLOPS,
-                "traffic": traffic,
-                "kernel": kname,
-                "note": "reference-algorithm-equivalent: FP64 flops F(k,p) of SURVEY.md 8(d) "
-                        "(13k^3 for dsyevd + the two k^3 products) per batch / HIP-event time "
-                        "of the batch's solve launches (rank 0); the kernels never form the "
-                        "eigendecomposition and execute fewer flops (executed); traffic: PMC "
-                        "HBM bytes of those launches",
-                "executed": executed,
-            },
+            "roofline": roof,
             "detail": {
                 "solver": "jacobi" if jacobi else "householder+quadrature",
+                "kernels_rank0": per_kernel,
                 "solved_per_step": solved / args.steps,
                 "ms_solve_per_step": ms_solve / args.steps,
                 "ms_search_per_step": ms_search / args.steps,
@@ -579,15 +738,16 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             # the reference's own compiled path when it travelled with the tree (built in
             # the container that has /root/reference), else the C restatement (port)
-            ref = cpu_baseline_reference(w)
-            port = cpu_baseline(w)
+            ref = guarded(cpu_baseline_reference, w)
+            port = guarded(cpu_baseline, w)
+            ref = ref if ref and "error" not in ref else None
             out["cpu_baseline"] = ref or port
             if ref:
                 out["detail"]["cpu_baseline_port"] = port
-            host = f"; host: {cpu_model()}, nproc {os.cpu_count()}, used {out['cpu_baseline']['cores']}"
-            for b in (ref, port):
-                if b:
-                    b["sample"] += host
+                # round 3's figure: 16 processes (the box's OMP_NUM_THREADS), for comparison
+                if ref["cores"] != 16:
+                    out["detail"]["cpu_baseline_16_procs"] = guarded(
+                        cpu_baseline_reference, w, procs=16)
         print(json.dumps(out), flush=True)
     core.finalize()
     if world > 1:

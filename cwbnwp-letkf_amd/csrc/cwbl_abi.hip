@@ -90,6 +90,13 @@ struct TreeBufs {
   }
 };
 
+enum KernelId {
+  KT_SEARCH_BINNED, KT_SEARCH_FLAGGED, KT_SEARCH_TREE, KT_ASSEMBLE_RECORD, KT_SOLVE_TQ40,
+  KT_BIG_HANDOFF, KT_TQB_TAIL, KT_SOLVE_TQ, KT_SOLVE_TQ_BIG, KT_SOLVE_JACOBI, KT_TUNE_Q,
+  KT_COUNT
+};
+struct KTime { long long launches = 0, points = 0; double ms = 0.0; };
+
 struct State {
   bool inited = false;
   int k = 0, kp = 0, device = 0, wf = 0, q1_mode = 0;
@@ -131,6 +138,15 @@ struct State {
   hipStream_t h2d = nullptr, d2h = nullptr;           // host-memory slab copies (pipelined)
   hipStream_t caller_stream = nullptr;                // cwbl_set_stream (null: legacy stream)
   hipEvent_t order_ev = nullptr;                      // order_after_caller
+  // cwbl_set_kernel_timing: every solve/search launch of cwbl_analyze_var bracketed by a HIP
+  // event pair on the stream it runs on; summed per kernel after the call's final sync
+  bool ktiming = false;
+  KTime ktime[KT_COUNT];
+  std::vector<hipEvent_t> kevents;
+  int kev_used = 0;
+  struct KPend { int id, ev; long long pts; };
+  std::vector<KPend> kpend;
+  size_t handoff_budget = 0;                          // bytes for the k > 64 hand-off records
 };
 
 State S;
@@ -198,6 +214,72 @@ float elapsed(int a, int b) {
   float ms = 0.0f;
   if (hipEventElapsedTime(&ms, S.events[a], S.events[b]) != hipSuccess) return 0.0f;
   return ms;
+}
+
+// Kernel timing (cwbl_set_kernel_timing): kt_begin records the first event of a launch's
+// pair on its stream (-1 when timing is off), kt_end the second, queued for kt_collect.
+hipError_t kt_event(int i, hipEvent_t *out) {
+  while ((int)S.kevents.size() <= i) {
+    hipEvent_t e;
+    hipError_t r = hipEventCreate(&e);
+    if (r != hipSuccess) return r;
+    S.kevents.push_back(e);
+  }
+  *out = S.kevents[i];
+  return hipSuccess;
+}
+
+hipError_t kt_begin(hipStream_t s, int *ev) {
+  *ev = -1;
+  if (!S.ktiming) return hipSuccess;
+  hipEvent_t e;
+  hipError_t r = kt_event(S.kev_used, &e);
+  if (r != hipSuccess) return r;
+  *ev = S.kev_used;
+  S.kev_used += 2;
+  return hipEventRecord(e, s);
+}
+
+hipError_t kt_end(hipStream_t s, int ev, int id, long long pts) {
+  if (ev < 0) return hipSuccess;
+  hipEvent_t e;
+  hipError_t r = kt_event(ev + 1, &e);
+  if (r != hipSuccess) return r;
+  S.kpend.push_back({id, ev, pts});
+  return hipEventRecord(e, s);
+}
+
+void kt_collect() {  // after the call's final synchronisation
+  for (const State::KPend &p : S.kpend) {
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, S.kevents[p.ev], S.kevents[p.ev + 1]) != hipSuccess) continue;
+    KTime &t = S.ktime[p.id];
+    t.launches += 1;
+    t.points += p.pts;
+    t.ms += ms;
+  }
+  S.kpend.clear();
+  S.kev_used = 0;
+}
+
+std::string kernel_name(int id) {
+  const std::string kp = std::to_string(S.kp);
+  switch (id) {
+    case KT_SEARCH_BINNED: return "search_binned_kernel";
+    case KT_SEARCH_FLAGGED: return "search_kernel<FlagQuery>";
+    case KT_SEARCH_TREE: return "search_kernel<SlabQuery>";
+    case KT_ASSEMBLE_RECORD: return "assemble_record_kernel<" + std::to_string(kRecordWaves) + ">";
+    case KT_SOLVE_TQ40: return "solve_tq40_kernel<" + kp + ", 0>";
+    case KT_BIG_HANDOFF:
+      return "solve_tq_big_kernel<" + kp + ", false, " + std::to_string(big_split_j0(S.kp)) + ">";
+    case KT_TQB_TAIL:
+      return "solve_tqb_tail_kernel<" + kp + ", " + std::to_string(big_split_j0(S.kp)) + ", 2>";
+    case KT_SOLVE_TQ: return "solve_tq_kernel<" + kp + ", false>";
+    case KT_SOLVE_TQ_BIG: return "solve_tq_big_kernel<" + kp + ", false>";
+    case KT_SOLVE_JACOBI: return "solve_kernel<" + kp + ", false>";
+    case KT_TUNE_Q: return "tune_q_kernel";
+  }
+  return "?";
 }
 
 int require_device() {
@@ -362,6 +444,12 @@ void release_all() {
     b->release();
   for (hipEvent_t e : S.events) (void)hipEventDestroy(e);
   S.events.clear();
+  for (hipEvent_t e : S.kevents) (void)hipEventDestroy(e);
+  S.kevents.clear();
+  S.kpend.clear();
+  S.kev_used = 0;
+  S.ktiming = false;
+  for (KTime &t : S.ktime) t = KTime{};
   if (S.order_ev) (void)hipEventDestroy(S.order_ev);
   S.order_ev = nullptr;
   S.caller_stream = nullptr;
@@ -389,11 +477,13 @@ SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps,
   c.nmember_inv = 1.0f / (float)S.k;
   c.r2 = search_r2();
   c.max_sweeps = 30;
-  if (const char *e = std::getenv("CWBL_DEBUG_MAX_SWEEPS")) c.max_sweeps = std::atoi(e);
   c.quad_r = S.quad.as<double2>();
   c.quad = c.quad_r;
+#ifdef CWBL_DEBUG_KNOBS  // timing ablations (make DEBUG_KNOBS=1); not in the release library
+  if (const char *e = std::getenv("CWBL_DEBUG_MAX_SWEEPS")) c.max_sweeps = std::atoi(e);
   if (const char *e = std::getenv("CWBL_DEBUG_TQ_STOP")) c.debug_stop = std::atoi(e);
   if (const char *e = std::getenv("CWBL_DEBUG_TQ_STEPS")) c.debug_steps = std::atoi(e);
+#endif
   return c;
 }
 
@@ -443,6 +533,13 @@ int cwbl_init(const cwbl_init_params *p) {
   S.norain = p->norain_value;
   S.q1_mode = p->q1_mode;
   S.ws_bytes = p->workspace_bytes ? p->workspace_bytes : (size_t(2) << 30);
+  if (p->workspace_bytes) {
+    S.handoff_budget = p->workspace_bytes;
+  } else {  // 13 GB (98 304 points at k = 128), at most 40% of what is free now
+    size_t fr = 0, tot = 0;
+    HIPCHK(hipMemGetInfo(&fr, &tot));
+    S.handoff_budget = std::min<size_t>((size_t)13 << 30, fr / 10 * 4);
+  }
   HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.sstream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.tstream, hipStreamNonBlocking));
@@ -476,7 +573,9 @@ int cwbl_init(const cwbl_init_params *p) {
   if (const char *e = std::getenv("CWBL_BIG_SUB")) S.big_sub = std::max(64LL, std::atoll(e));
   if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
   S.serial_search = false;
+#ifdef CWBL_DEBUG_KNOBS
   if (const char *e = std::getenv("CWBL_DEBUG_SERIAL")) S.serial_search = std::atoi(e) != 0;
+#endif
   // k = 17..32: the KP = 40 record path (assembly + four-point solve; the padding rows are
   // the identity and the steps past k - 2 exact no-ops) beats the one-wavefront KP = 24 / 32
   // solves (C2 grid, r2: 91.6 against 134 ms per variable at k = 32; r3: ~75 against 79 / 88
@@ -495,6 +594,34 @@ int cwbl_init(const cwbl_init_params *p) {
 int cwbl_set_stream(void *stream) {
   if (int rc = require_device()) return rc;
   S.caller_stream = static_cast<hipStream_t>(stream);
+  return CWBL_OK;
+}
+
+int cwbl_set_kernel_timing(int enable) {
+  if (int rc = require_device()) return rc;
+  S.ktiming = enable != 0;
+  for (KTime &t : S.ktime) t = KTime{};
+  return CWBL_OK;
+}
+
+int cwbl_kernel_times(cwbl_kernel_time *out, int cap, int *n) {
+  if (int rc = require_device()) return rc;
+  if (!n || cap < 0 || (cap > 0 && !out)) return fail(CWBL_ERR_ARG, "cwbl_kernel_times: bad arguments");
+  int m = 0;
+  for (int id = 0; id < KT_COUNT; ++id) {
+    const KTime &t = S.ktime[id];
+    if (t.launches == 0) continue;
+    if (m < cap) {
+      cwbl_kernel_time &o = out[m];
+      std::memset(&o, 0, sizeof o);
+      std::snprintf(o.name, sizeof o.name, "%s", kernel_name(id).c_str());
+      o.launches = t.launches;
+      o.points = t.points;
+      o.ms = t.ms;
+    }
+    ++m;
+  }
+  *n = m;
   return CWBL_OK;
 }
 
@@ -580,6 +707,8 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   if (!(vp->multi_infl > 0.0f)) return fail(CWBL_ERR_ARG, "multi_infl must be > 0");
   if (sl->memory == CWBL_MEM_DEVICE) HIPCHK(order_after_caller());
   const auto t_start = std::chrono::steady_clock::now();
+  S.kpend.clear();  // (an earlier call that failed midway leaves nothing to collect)
+  S.kev_used = 0;
   cwbl_stats st;
   std::memset(&st, 0, sizeof st);
   const long long npts = (long long)sl->ix_lim * sl->iy_lim * sl->nz;
@@ -729,16 +858,23 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     hipStream_t ss = S.serial_search ? S.stream : S.sstream;
     if (bi >= 2) HIPCHK(hipStreamWaitEvent(ss, S.events[done_ev[bi - 2]], 0));
     HIPCHK(hipEventRecord(a, ss));
+    int kt;
     if (S.binned) {  // bins; the tree search redoes the points whose lists pass max_lz
       int *fcnt = S.flags.as<int>(), *fidx = fcnt + 1;
       HIPCHK(hipMemsetAsync(fcnt, 0, sizeof(int), ss));
+      HIPCHK(kt_begin(ss, &kt));
       HIPCHK(launch_search_binned(ss, dtrees, nt, list_cap, c.r2, rbox, sd, g0, nb, ncnt, nidx,
                                   fcnt, fidx));
+      HIPCHK(kt_end(ss, kt, KT_SEARCH_BINNED, nb));
+      HIPCHK(kt_begin(ss, &kt));
       HIPCHK(launch_search_flagged(ss, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb, fcnt,
                                    fidx, ncnt, nidx, dst));
+      HIPCHK(kt_end(ss, kt, KT_SEARCH_FLAGGED, 0));
     } else {
+      HIPCHK(kt_begin(ss, &kt));
       HIPCHK(launch_search(ss, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb, ncnt,
                            nidx, nullptr, dst));
+      HIPCHK(kt_end(ss, kt, KT_SEARCH_TREE, nb));
     }
     HIPCHK(hipEventRecord(b, ss));
     HIPCHK(hipStreamWaitEvent(S.stream, b, 0));
@@ -756,28 +892,41 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       // 256-thread assembly + first kBigJ0 steps -> workspace -> one-wavefront tail, in
       // hand-off batches of Bs points (a multiple of kListLanes; BigHandoff<128, 64> is
       // 134.7 KB per point, 13 GB at the default 98 304, outside workspace_bytes)
-      const long long nsub = (nb + S.big_sub - 1) / S.big_sub;
+      // the sub-batch is also bounded by the hand-off budget (cwbl_init: workspace_bytes
+      // when the caller gave one, else 13 GB or 40% of the free device memory)
+      const size_t rec_bytes = (size_t)8 * (S.kp == 96 ? BigHandoff<96, 32>::WORDS
+                                                       : BigHandoff<kBigSplitKP, kBigJ0>::WORDS);
+      const long long fit = std::max<long long>(
+          kListLanes, (long long)(S.handoff_budget / rec_bytes) / kListLanes * kListLanes);
+      const long long cap = std::min<long long>(S.big_sub, fit);
+      const long long nsub = (nb + cap - 1) / cap;
       long long Bs = (nb + nsub - 1) / nsub;
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
-      HIPCHK(S.wsa.ensure((size_t)Bs * 8 *
-                          (S.kp == 96 ? BigHandoff<96, 32>::WORDS
-                                      : BigHandoff<kBigSplitKP, kBigJ0>::WORDS)));
+      HIPCHK(S.wsa.ensure((size_t)Bs * rec_bytes));
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
         const int ns = (int)std::min<long long>(Bs, nb - s0);
+        HIPCHK(kt_begin(S.stream, &kt));
         HIPCHK(launch_big_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,
                                   nidx + s0 * list_cap, S.info.as<int2>() + s0,
                                   S.wsa.as<double>()));
+        HIPCHK(kt_end(S.stream, kt, KT_BIG_HANDOFF, ns));
+        HIPCHK(kt_begin(S.stream, &kt));
         HIPCHK(launch_solve_tqb_tail(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
                                      S.info.as<int2>() + s0));
+        HIPCHK(kt_end(S.stream, kt, KT_TQB_TAIL, ns));
       }
-    } else if (S.kp > kMaxWaveKP)
+    } else if (S.kp > kMaxWaveKP) {
+      HIPCHK(kt_begin(S.stream, &kt));
       HIPCHK(launch_solve_tq_big(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
                                  nullptr, nullptr, nullptr, nullptr, nullptr,
                                  S.info.as<int2>()));
-    else if (S.jacobi)
+      HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ_BIG, nb));
+    } else if (S.jacobi) {
+      HIPCHK(kt_begin(S.stream, &kt));
       HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, ncnt, nidx,
                                     S.info.as<int2>()));
-    else if (S.tq4 && S.kp == kTq4KP) {
+      HIPCHK(kt_end(S.stream, kt, KT_SOLVE_JACOBI, nb));
+    } else if (S.tq4 && S.kp == kTq4KP) {
       // assembly -> workspace -> four-points-per-wave solve, in hand-off batches of Bs
       // points (a multiple of kListLanes, so a batch's neighbour lists start on a group)
       // (Bs <= 2^19: the solve addresses a batch's records with 32-bit byte offsets), the
@@ -800,31 +949,42 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
           double *recp = (nrec & 1) ? S.wsa2.as<double>() : S.wsa.as<double>();
           if (nrec >= 2)  // this record buffer: solved two record batches back
             HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[rec_done[nrec - 2]], 0));
+          HIPCHK(kt_begin(S.stream, &kt));
           HIPCHK(launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
                                         ncnt + s0 * nt, nidx + s0 * list_cap, binfo + s0,
                                         recp));
+          HIPCHK(kt_end(S.stream, kt, KT_ASSEMBLE_RECORD, ns));
           hipEvent_t ea, et;
           HIPCHK(cevent(cev, &ea));
           HIPCHK(cevent(cev + 1, &et));
           HIPCHK(hipEventRecord(ea, S.stream));
           HIPCHK(hipStreamWaitEvent(S.tstream, ea, 0));
+          HIPCHK(kt_begin(S.tstream, &kt));
           HIPCHK(launch_solve_tq40(S.tstream, S.kp, c, sd, g0 + s0, ns, recp, binfo + s0));
+          HIPCHK(kt_end(S.tstream, kt, KT_SOLVE_TQ40, ns));
           HIPCHK(hipEventRecord(et, S.tstream));
           rec_done.push_back(cev + 1);
           cev += 2;
           ++nrec;
         } else {
+          HIPCHK(kt_begin(S.stream, &kt));
           HIPCHK(launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
                                         ncnt + s0 * nt, nidx + s0 * list_cap,
                                         S.info.as<int2>() + s0, S.wsa.as<double>()));
+          HIPCHK(kt_end(S.stream, kt, KT_ASSEMBLE_RECORD, ns));
+          HIPCHK(kt_begin(S.stream, &kt));
           HIPCHK(launch_solve_tq40(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
                                    S.info.as<int2>() + s0));
+          HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ40, ns));
         }
       }
-    } else
+    } else {
+      HIPCHK(kt_begin(S.stream, &kt));
       HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
                              nullptr, nullptr, nullptr, nullptr, nullptr,
                              S.info.as<int2>()));
+      HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ, nb));
+    }
     HIPCHK(hipEventRecord(dn, S.stream));  // this batch's lists are free again
     if (conc) {  // the solves and the info reduction of this batch on S.tstream
       int2 *binfo = (bi & 1) ? S.info2.as<int2>() : S.info.as<int2>();
@@ -855,7 +1015,10 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     hipEvent_t a, b;
     HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b));
     HIPCHK(hipEventRecord(a, S.stream));
+    int kt;
+    HIPCHK(kt_begin(S.stream, &kt));
     HIPCHK(launch_tune_q(S.stream, sd, S.k));
+    HIPCHK(kt_end(S.stream, kt, KT_TUNE_Q, npts));
     HIPCHK(hipEventRecord(b, S.stream));
     solve_ev.push_back({ev, ev + 1});
     ev += 2;
@@ -873,6 +1036,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   DevStats ds;
   HIPCHK(hipMemcpyAsync(&ds, S.stats.p, sizeof ds, hipMemcpyDeviceToHost, S.stream));
   HIPCHK(hipStreamSynchronize(S.stream));
+  kt_collect();
 
   st.solved = (long long)ds.solved;
   st.nobs_sum = (long long)ds.nobs_sum;

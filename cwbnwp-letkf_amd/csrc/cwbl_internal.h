@@ -193,6 +193,7 @@ constexpr int kTq4KP = 40;  // KP of the split record path (k = 25..40)
 // J0..KP-1 plus the prefix rows' top-left block, then 16-lane rows of the trailing 32 x 32
 // matrix), solves and writes var in place.
 constexpr int kTq40J0 = 8;
+constexpr int kRecordWaves = 4;  // waves per SIMD of the record kernel (assemble_record_kernel)
 template <int KP>
 struct AsmRecord {
   static constexpr int TA = 0;                   // A(r, c), c <= r, at r (r + 1) / 2 + c

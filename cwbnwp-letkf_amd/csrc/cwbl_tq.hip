@@ -818,7 +818,6 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
   }
 }
 
-constexpr int kRecordWaves = 4;  // waves per SIMD of the record kernel
 
 hipError_t launch_assemble_record(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
                                   SlabDev slab, long long g0, int npts, const int *nbr_cnt,

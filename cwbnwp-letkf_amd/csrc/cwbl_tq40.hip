@@ -692,12 +692,15 @@ hipError_t launch_solve_tq40(hipStream_t s, int kp, SolveConsts c, SlabDev slab,
   if (npts <= 0) return hipSuccess;
   if (c.quad_r == nullptr || kp != kTq4KP) return hipErrorInvalidValue;
   const dim3 grid((npts + 3) / 4);
+#ifdef CWBL_DEBUG_KNOBS  // timing-ablation instantiations (make DEBUG_KNOBS=1)
   switch (c.debug_stop) {
-    case 2: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 2>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); break;
-    case 3: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 3>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); break;
-    case 4: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 4>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); break;
-    default: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info);
+    case 2: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 2>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
+    case 3: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 3>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
+    case 4: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 4>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
+    default: break;
   }
+#endif
+  hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info);
   return hipGetLastError();
 }
 

@@ -428,8 +428,12 @@ struct GtsLine {
   int qc[5] = {};
 };
 bool read_gts_line(std::istream &in, int nvar, GtsLine &g) {
-  static std::vector<Desc> fmt;
-  if (fmt.empty()) parse_format("(2i8,a5,2f9.2,f17.7,5(2f17.7,i8,2f17.7))", fmt);
+  // parsed once, thread-safely (a magic static): hosts may read member files concurrently
+  static const std::vector<Desc> fmt = [] {
+    std::vector<Desc> f;
+    parse_format("(2i8,a5,2f9.2,f17.7,5(2f17.7,i8,2f17.7))", f);
+    return f;
+  }();
   std::string line;
   if (!getline_rec(in, line)) return false;
   RecordReader r(line, fmt);
@@ -687,6 +691,9 @@ int cwbl_ingest_type_meta(cwbl_ingest *h, int family, int type_id, int *nvar, in
   if (!h) return ifail("cwbl_ingest_type_meta: null handle");
   if (family == 0 && type_id >= 1 && type_id <= CWBL_NUM_GTS_TYPES) {
     const GtsType &g = h->gts[type_id];
+    if (g.nobs > 0 && !g.meta)  // only member 0's file carries ids/lat/lon/alt (:508-611)
+      return ifail("cwbl_ingest_type_meta: GTS type %d has no metadata until member 0's file "
+                   "is read", type_id);
     if (nvar) *nvar = g.nvar;
     if (nobs) *nobs = std::max(g.nobs, 0);
     if (ids) *ids = g.ids.data();
@@ -697,6 +704,9 @@ int cwbl_ingest_type_meta(cwbl_ingest *h, int family, int type_id, int *nvar, in
   }
   if (family == 1 && type_id >= 1 && type_id <= CWBL_NUM_RADAR_TYPES) {
     const RadarType &r = h->radar[type_id];
+    if (r.nobs > 0 && !r.meta)  // only member 0's file carries lat/lon/alt (:120-186)
+      return ifail("cwbl_ingest_type_meta: radar type %d has no metadata until member 0's "
+                   "file is read", type_id);
     if (nvar) *nvar = 1;
     if (nobs) *nobs = std::max(r.nobs, 0);
     if (ids) *ids = nullptr;

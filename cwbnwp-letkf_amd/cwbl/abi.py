@@ -83,10 +83,15 @@ class Stats(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
 
 
+class KernelTime(C.Structure):
+    _fields_ = [("name", C.c_char * 64), ("launches", C.c_longlong), ("points", C.c_longlong),
+                ("ms", C.c_double)]
+
+
 #: exported symbols of the product library (include/cwb_letkf_core.h)
 EXPORTS = ["cwbl_init", "cwbl_set_stream", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch", "cwbl_search",
            "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
-           "cwbl_member_sum", "cwbl_scale",
+           "cwbl_member_sum", "cwbl_scale", "cwbl_set_kernel_timing", "cwbl_kernel_times",
            "cwbl_finalize", "cwbl_last_error", "cwbl_abi_version"]
 
 
@@ -261,12 +266,15 @@ def load_library(path=None):
     lib.cwbl_vcoord_mean.argtypes = [vp, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_float, vp]
     lib.cwbl_member_sum.argtypes = [vp, C.c_longlong, C.c_int, vp]
     lib.cwbl_scale.argtypes = [vp, C.c_longlong, C.c_float]
+    lib.cwbl_set_kernel_timing.argtypes = [C.c_int]
+    lib.cwbl_kernel_times.argtypes = [C.POINTER(KernelTime), C.c_int, C.POINTER(C.c_int)]
     lib.cwbl_finalize.argtypes = []
     lib.cwbl_last_error.restype = cp
     lib.cwbl_abi_version.restype = C.c_int
     for fn in ("cwbl_init", "cwbl_set_stream", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch",
                "cwbl_search", "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
-               "cwbl_member_sum", "cwbl_scale", "cwbl_finalize"):
+               "cwbl_member_sum", "cwbl_scale", "cwbl_set_kernel_timing", "cwbl_kernel_times",
+               "cwbl_finalize"):
         getattr(lib, fn).restype = C.c_int
     return lib
 
@@ -353,6 +361,19 @@ class Core:
     def scale(self, x, n, alpha):
         """sscal (module_grid.f90:827-...)."""
         self._check(self.lib.cwbl_scale(_ptr(x), n, alpha))
+
+    def set_kernel_timing(self, enable=True):
+        """HIP-event timing of every search/solve launch of analyze_var, on the launch's own
+        stream; clears the sums."""
+        self._check(self.lib.cwbl_set_kernel_timing(int(enable)))
+
+    def kernel_times(self):
+        """{kernel name: {launches, points, ms}} summed since set_kernel_timing."""
+        cap, n = 32, C.c_int(0)
+        buf = (KernelTime * cap)()
+        self._check(self.lib.cwbl_kernel_times(buf, cap, C.byref(n)))
+        return {buf[i].name.decode(): {"launches": buf[i].launches, "points": buf[i].points,
+                                       "ms": buf[i].ms} for i in range(min(n.value, cap))}
 
     def finalize(self):
         self._check(self.lib.cwbl_finalize())

@@ -372,5 +372,12 @@ def var_params(cfg, ivar):
 
 
 def var_names(cfg):
-    """The var_update entries (blank entries dropped), 1-based position = ivar."""
-    return [v.strip() for v in cfg["control"]["var_update"] if v.strip()]
+    """The var_update entries up to the first blank one, 1-based position = ivar: letkf_driver
+    leaves its variable loop at the first blank entry (module_letkf_core.f90:59-60,
+    `if(len_trim(var_update(ivar)) == 0) exit`), so names after a gap are never analysed."""
+    out = []
+    for v in cfg["control"]["var_update"]:
+        if not v.strip():
+            break
+        out.append(v.strip())
+    return out

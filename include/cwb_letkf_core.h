@@ -33,10 +33,12 @@
  *  - All calls are synchronous, from one host thread per process; `memory` says whether
  *    the array pointers of a struct are host pointers (copied in/out inside the call) or
  *    HIP device pointers already resident on the library's device.
- *  - Device inputs only need to be *queued*: every call that takes device pointers first
- *    waits for all work already queued on the device by this process (any stream: the null
- *    stream, torch's current stream, an RCCL broadcast), and all library work on those
- *    buffers has completed when the call returns.
+ *  - Device inputs only need to be *queued* on the caller's stream (cwbl_set_stream; the
+ *    legacy null stream by default): every call that takes device pointers first makes the
+ *    library's streams wait for an event recorded there, so work queued on OTHER streams
+ *    (torch's non-default streams, an RCCL collective's stream) must be complete or ordered
+ *    before that stream by the caller.  All library work on those buffers has completed when
+ *    the call returns.
  *  - Return value 0 = success; nonzero = error code, message in cwbl_last_error().
  *  - There is no CPU fallback: without a usable gfx950 device every compute entry point
  *    returns CWBL_ERR_NO_DEVICE.
@@ -95,9 +97,10 @@ typedef struct cwbl_init_params {
   int    reserved;
   size_t workspace_bytes;  /* device workspace budget for neighbour lists (0 = 2 GiB); the
                             * solve's per-batch records come on top: 6.9 KB per point of a
-                            * search batch at k = 25..40 (two buffers), 135 KB per point of a
-                            * k = 65..128 hand-off sub-batch (CWBL_BIG_SUB, at most 98 304 points:
-                            * up to 13 GB) */
+                            * search batch at k = 17..40 (two buffers); at k = 65..128 the
+                            * hand-off records (135 KB per point) are bounded by this value
+                            * when it is given, else by min(13 GB, 40% of the device memory
+                            * free at cwbl_init), with sub-batches shrunk to fit */
 } cwbl_init_params;
 
 /* One GTS platform: type(gts_structure), module_gts_omboma.f90:13-22. */
@@ -256,6 +259,21 @@ int         cwbl_vcoord_mean(const float *ph, long long n2d, int nz_ph, int k, i
 int         cwbl_member_sum(const float *fields, long long n, int nm, float *out);
 /* x(i) = alpha * x(i) (sscal, :827-...). */
 int         cwbl_scale(float *x, long long n, float alpha);
+
+/* ---- kernel timing (measurement; no reference counterpart) -------------------------------
+ * With timing on, cwbl_analyze_var brackets every search and solve launch with a HIP event
+ * pair on the stream the launch runs on and, after the call's final synchronisation, adds
+ * the pair's elapsed time to that kernel's sum.  cwbl_set_kernel_timing(1) switches timing
+ * on and clears the sums (0 switches it off); cwbl_kernel_times copies up to `cap` entries,
+ * one per kernel launched since, and stores the number of such kernels in *n. */
+typedef struct cwbl_kernel_time {
+  char      name[64];   /* the kernel as rocprofv3 names it, template arguments included */
+  long long launches;
+  long long points;     /* grid points the launches processed (0: flagged-point re-search) */
+  double    ms;         /* summed HIP-event time */
+} cwbl_kernel_time;
+int         cwbl_set_kernel_timing(int enable);
+int         cwbl_kernel_times(cwbl_kernel_time *out, int cap, int *n);
 
 int         cwbl_finalize(void);
 const char *cwbl_last_error(void);

@@ -68,7 +68,9 @@ int cwbl_ingest_read_radar(cwbl_ingest *h, int member, const char *file, const c
 int cwbl_ingest_obs_set(cwbl_ingest *h, cwbl_obs_set *out);
 
 /* Per-type metadata the obs set does not carry: station ids (5 characters per obs, not NUL
- * terminated) and lat, lon, alt (degrees, degrees, metres).  family 0 GTS, 1 radar (ids NULL). */
+ * terminated) and lat, lon, alt (degrees, degrees, metres).  family 0 GTS, 1 radar (ids NULL).
+ * Only member 0's file fills them (the root reader, module_gts_omboma.f90:508-611): a type
+ * read from other members' files alone returns CWBL_ERR_ARG here. */
 int cwbl_ingest_type_meta(cwbl_ingest *h, int family, int type_id, int *nvar, int *nobs,
                           const char **ids, const float **lat, const float **lon,
                           const float **alt);

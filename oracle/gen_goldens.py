@@ -350,11 +350,14 @@ def main():
     if not os.path.exists(HARNESS):
         sys.exit("build oracle/_ref/ref_harness first (make -C oracle ref)")
     os.makedirs(OUT, exist_ok=True)
-    manifest = {"provenance": "reference modules param/config/eigen/kdtree2 + source text of "
-                "letkf_solve and Gaspari_Cohn_1999 compiled by oracle/ref/build_ref.sh with "
-                "amdflang 22 -O2 (x86-64, no FMA), MKL libmkl_rt (sequential, MKL_CBWR="
-                "COMPATIBLE), glibc 2.35 expf (FMA IFUNC variant); driver glue restated in "
-                "oracle/ref/ref_driver.inc", "files": {}}
+    manifest = {"provenance": "reference modules param/config/eigen/kdtree2 (Q7: one array "
+                "section of kdtree2_create made explicit) and localization (build_tree, get_lz, "
+                "Gaspari_Cohn_1999) on type-only gts_omboma/simulated_radar modules cut from "
+                "the reference, + source text of letkf_yoyb, letkf_solve and letkf_tune_q, "
+                "compiled by oracle/ref/build_ref.sh with amdflang 22 -O2 (x86-64, no FMA), MKL "
+                "libmkl_rt (sequential, MKL_CBWR=COMPATIBLE), glibc 2.35 expf (FMA IFUNC "
+                "variant); only letkf_driver's point loop (module_letkf_core.f90:209-240) is "
+                "written out, in oracle/ref/ref_driver.inc", "files": {}}
 
     raw = run("consts", b"")
     c = np.frombuffer(raw, f4)

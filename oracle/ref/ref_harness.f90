@@ -3,10 +3,10 @@
 ! TEST INFRASTRUCTURE ONLY (built by oracle/ref/build_ref.sh into oracle/_ref/).
 ! Real reference code exercised: module param / config (read_namelist) / eigen
 ! (set_optimal_workspace_for_eigen, inverse_matrix, sqrt_matrix) / kdtree2_module
-! (kdtree2_create, kdtree2_r_nearest) and the source text of letkf_solve, letkf_tune_q and
-! Gaspari_Cohn_1999.  The glue that the reference keeps in modules we cannot compile here
-! (build_tree/get_lz normalisation, letkf_yoyb, the driver loop) is restated below,
-! line for line, with the file:line it follows.
+! (kdtree2_create, kdtree2_r_nearest) / localization (build_tree, get_lz, destroy_tree,
+! Gaspari_Cohn_1999) and the source text of letkf_yoyb, letkf_solve and letkf_tune_q (see
+! build_ref.sh).  Only letkf_driver's point loop (module_letkf_core.f90:209-240) is written
+! out here (ref_driver.inc); letkf_driver itself needs the MPI decomposition.
 !
 ! Usage: ref_harness <mode> <in.bin> <out.bin>,
 ! modes: consts | solve | search | gc | driver | tuneq | ingest
@@ -21,6 +21,7 @@ module harness_lib
     use ref_extract
     use projection, only : proj_type
     use ref_ingest
+    use localization, only : lz_structure, build_tree, get_lz, destroy_tree, Gaspari_Cohn_1999
     implicit none
 
     character(len=512) :: fin, fout
@@ -101,68 +102,52 @@ contains
         close(21)
     end subroutine do_solve
 
-    ! get_lz KATs for a single obs type (no Q1 mixing).
+    ! get_lz KATs for a single obs type (no Q1 mixing), through the reference's compiled
+    ! build_tree / get_lz (module_localization.f90:35-167, 188-331): the points are the vr
+    ! radar type (module_radar.f90:13-16), whose namelist entries (radar_nml%vr%use_it,
+    ! %max_lz_pts, %hclr(1), %vclr(1)) go through read_namelist.
     ! in: nobs nq max_lz (i4) hclr vclr (r4) xyz(3,nobs) q(3,nq) (r4)
     ! out: per query nfound (i4) idx(max_lz) (i4, 1-based, 0 padded) r2(max_lz) (r4)
     subroutine do_search
-        integer :: nobs, nq, max_lz, dim, iq, nlz
-        real    :: hclr, vclr, hclr_inv, vclr_inv
-        real, parameter :: r2 = gc1999 * gc1999             ! module_localization.f90:202
-        real, allocatable :: xyz(:,:), q(:,:)
-        real    :: tmp(3)
-        type(kdtree2), pointer :: tree
-        type(kdtree2_result), allocatable :: results(:)
+        integer :: nobs, nq, max_lz, iq, nlz
+        real    :: hclr, vclr
+        real, allocatable :: q(:,:)
+        type(cwb_radar) :: rad
+        type(lz_structure), dimension(:), allocatable :: lz
         integer, allocatable :: idx(:)
         real,    allocatable :: dis(:)
+        character(len=400) :: obsl
+        logical :: ok, fail
         open(40, file=trim(fin), access='stream', form='unformatted', status='old')
         read(40) nobs, nq, max_lz
         read(40) hclr, vclr
-        allocate(xyz(3,nobs), q(3,nq), results(max_lz), idx(max_lz), dis(max_lz))
-        read(40) xyz, q
+        allocate(rad%radarobs(num_radar_indexes))
+        rad%radarobs(vr)%nobs = nobs
+        allocate(rad%radarobs(vr)%xyz(3,nobs), q(3,nq), idx(max_lz), dis(max_lz))
+        read(40) rad%radarobs(vr)%xyz, q
         close(40)
-        ! build_tree normalisation, module_localization.f90:76-82, 148-160
-        hclr_inv = 1.0 / (hclr * 1e3)
-        if (vclr > 0.) then
-            vclr_inv = 1.0 / (vclr * 1e3)
-        else
-            vclr_inv = -1.
-        end if
-        xyz(1:2,:) = xyz(1:2,:) * hclr_inv
-        if (vclr_inv > 0.) then
-            dim = 3
-            xyz(3,:) = xyz(3,:) * vclr_inv
-        else
-            dim = 2
-            xyz(3,:) = -1.
-        end if
-        ! Q7: with dim = 2, kdtree2_create copies the_data(:,ind(i)) (3 rows) into
-        ! rearranged_data(2,n) (module_kdtree2.f90:671-675) — flang's runtime rejects that
-        ! shape mismatch, so pass the two rows the tree actually reads (same tree, same search).
-        if (dim == 3) then
-            tree => kdtree2_create(xyz, dim=dim)
-        else
-            tree => kdtree2_create(xyz(1:2,:), dim=dim)
-        end if
+        write(obsl, '(a,i0,a,es16.8e3,a,es16.8e3)') ' radar_nml%vr%use_it = T'//char(10)// &
+            ' radar_nml%vr%max_lz_pts = ', max_lz, char(10)//' radar_nml%vr%hclr(1) = ', hclr, &
+            char(10)//' radar_nml%vr%vclr(1) = ', vclr
+        call setup_k(8, obsl=trim(obsl))
+        ok = build_tree(rad % radarobs, 1)
+        if (.not. ok) stop "do_search: build_tree built no tree"
         open(21, file=trim(fout), access='stream', form='unformatted', status='replace')
         do iq = 1, nq
-            ! get_lz, module_localization.f90:243-253
-            tmp(1:2) = q(1:2,iq) * hclr_inv
-            if (vclr_inv > 0.) then
-                tmp(3) = q(3,iq) * vclr_inv
-                call kdtree2_r_nearest(tree, tmp(1:3), r2, nlz, max_lz, results)
-            else
-                call kdtree2_r_nearest(tree, tmp(1:2), r2, nlz, max_lz, results)
-            end if
+            fail = get_lz('radar', lz, 1, q(:,iq))
             idx = 0
             dis = 0.
-            if (nlz > 0) then
-                idx(1:nlz) = results(1:nlz) % idx
-                dis(1:nlz) = results(1:nlz) % dis
+            nlz = 0
+            if (.not. fail) then
+                nlz = size(lz(1) % idx)
+                idx(1:nlz) = lz(1) % idx
+                dis(1:nlz) = lz(1) % r2
             end if
             write(21) nlz, idx, dis
+            if (allocated(lz)) deallocate(lz)
         end do
         close(21)
-        call kdtree2_destroy(tree)
+        call destroy_tree
     end subroutine do_search
 
     subroutine do_gc

@@ -2,6 +2,7 @@
 # solve_tq40_kernel time split on the C2 bench (CWBL_DEBUG_TQ_STOP ablations: 4 = phase 1
 # only, 2 = + phase 2 (the whole tridiagonalisation), 3 = + quadrature, 0 = whole kernel),
 # kernel statistics per ablation -> gpurun_out/tq40_ablate/<stop>/
+# (needs the library built with the knobs: make -C cwbnwp-letkf_amd DEBUG_KNOBS=1 clean all)
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp CWBL_TQ40_STREAMS=0
 OUT=gpurun_out/tq40_ablate

@@ -58,7 +58,7 @@ STRUCTS = {
     "cwbl_init_params": abi.InitParams, "cwbl_gts_obs": abi.GtsObs,
     "cwbl_radar_obs": abi.RadarObs, "cwbl_obs_set": abi.ObsSet,
     "cwbl_type_params": abi.TypeParams, "cwbl_var_params": abi.VarParams,
-    "cwbl_slab": abi.Slab, "cwbl_stats": abi.Stats,
+    "cwbl_slab": abi.Slab, "cwbl_stats": abi.Stats, "cwbl_kernel_time": abi.KernelTime,
 }
 
 

@@ -129,6 +129,20 @@ def test_metadata_comes_from_member_0(tmp_path):
     np.testing.assert_array_equal(a.meta(1, abi.RADAR_VR)["lon"], b.meta(1, abi.RADAR_VR)["lon"])
 
 
+def test_metadata_before_member_0_is_an_error():
+    """A host that has read only member 1's files has hdxb/qc but no metadata (the root
+    reader's arrays): meta() must fail, not hand out pointers into empty buffers."""
+    h = ingest.Ingest(3)
+    h.read_radar(os.path.join(DIR, "VR_letkf_002"), "VR")
+    h.read_gts(os.path.join(DIR, "gts_letkf_002"), os.path.join(DIR, "obs_gts"))
+    with pytest.raises(abi.CwblError, match="no metadata"):
+        h.meta(1, abi.RADAR_VR)
+    with pytest.raises(abi.CwblError, match="no metadata"):
+        h.meta(0, abi.GTS_SYNOP)
+    h.read_radar(os.path.join(DIR, "VR_letkf_001"), "VR")
+    assert h.meta(1, abi.RADAR_VR)["lon"].size > 0
+
+
 def test_errors_are_reported_not_ignored(tmp_path):
     d = tmp_path / "in"
     shutil.copytree(DIR, d)

@@ -173,3 +173,11 @@ def test_var_params_feed_the_core_types():
     assert q.tune_q == 1 and q.radar[abi.RADAR_DBZ - 1].hclr == 8.0
     p = namelist.projection(cfg)
     assert (p.sta_lon, p.truelat1, p.truelat2) == (120.0, 10.0, 40.0)
+
+
+def test_var_names_stop_at_the_first_blank_entry():
+    """letkf_driver exits its variable loop at the first blank var_update entry
+    (module_letkf_core.f90:59-60): the EDGE namelist has a null value after 2*'QRAIN', so
+    'P' is never analysed and ivar positions are not shifted."""
+    cfg = namelist.read_namelist(EDGE, is_text=True)
+    assert namelist.var_names(cfg) == ["U", "V", "QRAIN", "QRAIN"]
