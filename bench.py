@@ -181,7 +181,15 @@ def cpu_baseline_reference(w, target_s=12.0, procs=None):
         dt, pts = run(nb, procs)
         if dt >= 0.7 * target_s or nb >= nb_max:
             break
+    n_aff, n_phys, quota = host_cores()
     return {"value": pts / dt, "unit": "grid-points/s", "cores": procs, "kind": "reference",
+            "per_core": pts / dt / procs,
+            "physical_cores_in_affinity": n_phys,
+            "extrapolated_all_physical_cores": pts / dt / procs * n_phys,
+            "extrapolation_note": "per-core rate x the physical cores of the affinity set, for "
+                                  "comparison only: the job's cgroup quota caps what can run "
+                                  "at once" if quota is not None and quota < n_phys else
+                                  "all physical cores were timed",
             "sample": f"{procs} single-threaded processes (the reference's flat MPI layout), "
                       f"each {nb}x{nb} columns x {w.nz} levels of the {w.name} grid: {pts} points "
                       f"in {dt:.1f} s; reference letkf_solve/kdtree2/read_namelist compiled with "
@@ -307,7 +315,7 @@ def time_cycle(core, w, rank, world, dev, x, y, alt, transposes=True):
         per[name] = round((td - ta) * 1e3, 2)
     tm = time.perf_counter()
     if transposes:  # write_mean: every analysed field of the owned members, one reduce
-        t.write_mean({m: [fields[kind][m] for _, _, kind in runs] for m in t.owned()})
+        t.write_mean({m: [fields[kind][m] for _, kind, _ in runs] for m in t.owned()})
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     vals = _max_over_ranks([(t1 - t0) * 1e3, ms_sc, ms_an, ms_ga, (t1 - tm) * 1e3], world, dev)

@@ -14,6 +14,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -67,6 +71,106 @@ struct DevBuf {
   template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+// grow-only page-locked host buffer (bounce slots of pageable host slabs)
+struct PinBuf {
+  void *p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e == hipSuccess) n = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+// A few persistent host threads for the bounce copies: run(n, fn) calls fn(0..n-1) spread
+// over the threads and the caller, and returns when all calls are done.
+class HostPool {
+ public:
+  ~HostPool() { stop(); }
+  void run(int n, const std::function<void(int)> &fn) {
+    if (n <= 0) return;
+    start();
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_ = 0;
+      busy_ = (int)th_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return busy_ == 0; });
+    fn_ = nullptr;
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      quit_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+    th_.clear();
+    quit_ = false;
+  }
+
+ private:
+  void start() {
+    if (!th_.empty()) return;
+    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    int nt = (int)std::min(15u, hw - 1);  // + the calling thread: at most 16
+    if (const char *e = std::getenv("OMP_NUM_THREADS"))
+      nt = std::max(0, std::min(nt, std::atoi(e) - 1));
+    for (int i = 0; i < nt; ++i) th_.emplace_back([this] { loop(); });
+  }
+  void work() {
+    for (;;) {
+      int i;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!fn_ || next_ >= n_) return;
+        i = next_++;
+      }
+      (*fn_)(i);
+    }
+  }
+  void loop() {
+    unsigned long seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (quit_) return;
+      }
+      work();
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (--busy_ == 0) done_.notify_all();
+      }
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)> *fn_ = nullptr;
+  int n_ = 0, next_ = 0, busy_ = 0;
+  unsigned long gen_ = 0;
+  bool quit_ = false;
+};
+
 struct ObsType {
   int family = 0, type_id = 0, nvar = 1, nobs = 0;
   std::vector<float> xyz;   // host copy (3,nobs) for tree builds
@@ -110,7 +214,7 @@ struct State {
   DevBuf nbr_cnt2, nbr_idx2;                          // second list buffer (search overlap)
   hipStream_t sstream = nullptr;                      // neighbour searches of later batches
   hipStream_t tstream = nullptr;                      // solve_tq40_kernel (record path)
-  bool tq40_streams = true;  // CWBL_TQ40_STREAMS=0: solve_tq40_kernel on S.stream (no overlap)
+  bool tq40_streams = false;  // CWBL_TQ40_STREAMS=1: solve_tq40_kernel on its own stream
   DevBuf wsa2, info2;                                 // second record / info buffers
   std::vector<hipEvent_t> cevents;                    // record-path events (cevent)
   int lead_div = 0;                                   // first batch = npts / lead_div (0: off)
@@ -147,6 +251,11 @@ struct State {
   struct KPend { int id, ev; long long pts; };
   std::vector<KPend> kpend;
   size_t handoff_budget = 0;                          // bytes for the k > 64 hand-off records
+  // pageable host slabs: each batch's var columns go through page-locked bounce slots (two
+  // in, two out), filled and drained by a few host threads while the GPU runs other batches
+  static constexpr int kSlots = 3;
+  PinBuf pin_in[kSlots], pin_out[kSlots];
+  HostPool pool;
 };
 
 State S;
@@ -280,6 +389,30 @@ std::string kernel_name(int id) {
     case KT_TUNE_Q: return "tune_q_kernel";
   }
   return "?";
+}
+
+// page-locked (hipHostMalloc'd or hipHostRegister'ed) host memory: DMA-able as it is
+bool host_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// k rows of nb floats between a member-slowest host slab (row pitch L) and a packed slot
+double g_bounce_ms = 0.0;  // host time in the bounce copies of the current call
+void bounce_rows(HostPool &pool, float *slot, float *var, long long L, long long g0, int nb,
+                 int k, bool to_slot) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t row = (size_t)nb * 4;
+  pool.run(k, [&](int m) {
+    float *h = var + (size_t)m * L + g0, *b = slot + (size_t)m * nb;
+    if (to_slot) std::memcpy(b, h, row);
+    else std::memcpy(h, b, row);
+  });
+  g_bounce_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 int require_device() {
@@ -446,6 +579,11 @@ void release_all() {
   S.events.clear();
   for (hipEvent_t e : S.kevents) (void)hipEventDestroy(e);
   S.kevents.clear();
+  for (int i = 0; i < State::kSlots; ++i) {
+    S.pin_in[i].release();
+    S.pin_out[i].release();
+  }
+  S.pool.stop();
   S.kpend.clear();
   S.kev_used = 0;
   S.ktiming = false;
@@ -560,7 +698,10 @@ int cwbl_init(const cwbl_init_params *p) {
   S.tq4 = 1;
   if (const char *e = std::getenv("CWBL_TQ4")) S.tq4 = std::atoi(e);
   if (const char *e = std::getenv("CWBL_TQ4_SUB")) S.tq4_sub = std::atoll(e);
-  S.tq40_streams = true;
+  // r4: one stream by default.  With the r3 kernels the two-stream record path measures a
+  // tie (C2 58.7-59.2 M pts/s either way), and serial launches keep each
+  // kernel's duration its own (the per-kernel timing and the roofline read it).
+  S.tq40_streams = false;
   if (const char *e = std::getenv("CWBL_TQ40_STREAMS")) S.tq40_streams = std::atoi(e) != 0;
   S.big_split = true;
   // (C4 per variable, r3: 32 k points 2.42 s, 16 k 2.47, 64 k 2.41, 96 k 2.39, 128 k 2.39)
@@ -709,6 +850,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   const auto t_start = std::chrono::steady_clock::now();
   S.kpend.clear();  // (an earlier call that failed midway leaves nothing to collect)
   S.kev_used = 0;
+  g_bounce_ms = 0.0;
   cwbl_stats st;
   std::memset(&st, 0, sizeof st);
   const long long npts = (long long)sl->ix_lim * sl->iy_lim * sl->nz;
@@ -758,13 +900,17 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   const bool host = sl->memory != CWBL_MEM_DEVICE;
   const bool piped = host && sl->ix_lim == sl->nx && sl->iy_lim == sl->ny;
   const bool piped_back = piped && !vp->tune_q;  // tune_q touches the whole slab afterwards
+  // pageable var (a Fortran host's ordinary arrays): copies from pageable memory are staged
+  // by the runtime and do not overlap, so var goes through the library's page-locked bounce
+  // slots instead, filled / drained by host threads while the GPU runs other batches
+  const bool bounce = host && bvar > 0 && !host_pinned(sl->var);
   if (!host) {
     sd.x = sl->x; sd.y = sl->y; sd.alt = sl->alt; sd.var = sl->var;
   } else {
     HIPCHK(stage(S.sx, sl->x, bxy, CWBL_MEM_HOST));
     HIPCHK(stage(S.sy, sl->y, bxy, CWBL_MEM_HOST));
     HIPCHK(stage(S.salt, sl->alt, balt, CWBL_MEM_HOST));
-    if (piped) HIPCHK(S.svar.ensure(bvar));
+    if (piped || bounce) HIPCHK(S.svar.ensure(bvar));
     else HIPCHK(stage(S.svar, sl->var, bvar, CWBL_MEM_HOST));
     sd.x = S.sx.as<float>(); sd.y = S.sy.as<float>(); sd.alt = S.salt.as<float>();
     sd.var = S.svar.as<float>();
@@ -801,6 +947,71 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     for (const auto &b : plan) B = std::max<long long>(B, b.second);
   }
   const long long nbat = (long long)plan.size();
+  // bounce slots: one batch (or one whole-slab chunk of B points) of k member rows each
+  const long long Bc = std::min<long long>(std::max<long long>(B, 1), std::max<long long>(L, 1));
+  int cev = 0;
+  std::vector<int> h2d_done, d2h_done;  // cevents of the bounce copies
+  // whole-slab moves through the slots (var not piped, or back after tune_q): chunk i of Bc
+  // points of every member row; up: fill slot i&1 (after its copy two chunks back), copy up on
+  // S.stream; down: copy chunk i down on S.stream, then drain chunk i-1 while it runs
+  auto bounce_whole = [&](bool up) -> int {
+    std::vector<int> evs;
+    long long pc0 = 0;
+    int pcn = 0;
+    const size_t pitch = (size_t)L * 4;
+    for (long long c0 = 0, i = 0; c0 < L; c0 += Bc, ++i) {
+      const int cn = (int)std::min<long long>(Bc, L - c0);
+      PinBuf &slot = up ? S.pin_in[i & 1] : S.pin_out[i & 1];
+      hipEvent_t e;
+      HIPCHK(cevent(cev, &e));
+      if (up) {
+        if (i >= 2) HIPCHK(hipEventSynchronize(S.cevents[evs[(size_t)i - 2]]));
+        bounce_rows(S.pool, slot.as<float>(), sl->var, L, c0, cn, S.k, true);
+        HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + c0, pitch, slot.p, (size_t)cn * 4,
+                                (size_t)cn * 4, (size_t)S.k, hipMemcpyHostToDevice, S.stream));
+      } else {
+        HIPCHK(hipMemcpy2DAsync(slot.p, (size_t)cn * 4, S.svar.as<float>() + c0, pitch,
+                                (size_t)cn * 4, (size_t)S.k, hipMemcpyDeviceToHost, S.stream));
+      }
+      HIPCHK(hipEventRecord(e, S.stream));
+      evs.push_back(cev++);
+      if (!up && i >= 1) {
+        HIPCHK(hipEventSynchronize(S.cevents[evs[(size_t)i - 1]]));
+        bounce_rows(S.pool, S.pin_out[(i - 1) & 1].as<float>(), sl->var, L, pc0, pcn, S.k, false);
+      }
+      pc0 = c0;
+      pcn = cn;
+    }
+    if (!up && !evs.empty()) {
+      HIPCHK(hipEventSynchronize(S.cevents[evs.back()]));
+      bounce_rows(S.pool, S.pin_out[(evs.size() - 1) & 1].as<float>(), sl->var, L, pc0, pcn,
+                  S.k, false);
+    }
+    return CWBL_OK;
+  };
+  if (bounce) {
+    const size_t slot_bytes = (size_t)Bc * S.k * 4;
+    for (int i = 0; i < State::kSlots; ++i) {
+      HIPCHK(S.pin_in[i].ensure(slot_bytes));
+      HIPCHK(S.pin_out[i].ensure(slot_bytes));
+    }
+    if (!piped)
+      if (int rc = bounce_whole(true)) return rc;
+  }
+  // piped bounce: batch b's columns into slot b % kSlots once the copy up of batch
+  // b - kSlots has left it; batch b's analysis out of its slot once its copy down is done
+  auto bounce_fill = [&](long long b) -> int {
+    if (b >= State::kSlots) HIPCHK(hipEventSynchronize(S.cevents[h2d_done[b - State::kSlots]]));
+    bounce_rows(S.pool, S.pin_in[b % State::kSlots].as<float>(), sl->var, L, plan[b].first,
+                plan[b].second, S.k, true);
+    return CWBL_OK;
+  };
+  auto bounce_drain = [&](long long b) -> int {
+    HIPCHK(hipEventSynchronize(S.cevents[d2h_done[b]]));
+    bounce_rows(S.pool, S.pin_out[b % State::kSlots].as<float>(), sl->var, L, plan[b].first,
+                plan[b].second, S.k, false);
+    return CWBL_OK;
+  };
   const size_t bytes_cnt = (size_t)B * nt * 4;
   const size_t bytes_idx =
       (size_t)((B + kListLanes - 1) / kListLanes) * kListLanes * std::max(list_cap, 1) * 4;
@@ -843,7 +1054,6 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   int nrec = 0;                 // record batches so far
   std::vector<int> rec_done;    // cevent after each record batch's solve (on S.tstream)
   std::vector<int> info_done;   // cevent after each search batch's info reduction
-  int cev = 0;
   if (conc) HIPCHK(S.info2.ensure((size_t)B * sizeof(int2)));
   for (long long bi = 0; bi < nbat; ++bi) {
     const long long g0 = plan[bi].first;
@@ -880,11 +1090,21 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     HIPCHK(hipStreamWaitEvent(S.stream, b, 0));
     if (piped) {  // this batch's var columns: k rows of nb floats, member pitch L
       hipEvent_t hv;
-      HIPCHK(cevent(cev++, &hv));
+      const int hv_i = cev++;
+      HIPCHK(cevent(hv_i, &hv));
       const size_t pitch = (size_t)L * 4;
-      HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + g0, pitch, sl->var + g0, pitch,
-                              (size_t)nb * 4, (size_t)S.k, hipMemcpyHostToDevice, S.h2d));
+      if (bounce) {  // slot bi % kSlots, filled before this batch (bounce_fill)
+        if (bi == 0)
+          if (int rc = bounce_fill(0)) return rc;
+        HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + g0, pitch,
+                                S.pin_in[bi % State::kSlots].p, (size_t)nb * 4, (size_t)nb * 4,
+                                (size_t)S.k, hipMemcpyHostToDevice, S.h2d));
+      } else {
+        HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + g0, pitch, sl->var + g0, pitch,
+                                (size_t)nb * 4, (size_t)S.k, hipMemcpyHostToDevice, S.h2d));
+      }
       HIPCHK(hipEventRecord(hv, S.h2d));
+      h2d_done.push_back(hv_i);
       HIPCHK(hipStreamWaitEvent(S.stream, hv, 0));
     }
     HIPCHK(hipEventRecord(b2, S.stream));
@@ -1001,8 +1221,25 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     if (piped_back) {  // the batch's analysis back to the caller behind its last solve
       HIPCHK(hipStreamWaitEvent(S.d2h, cc, 0));
       const size_t pitch = (size_t)L * 4;
-      HIPCHK(hipMemcpy2DAsync(sl->var + g0, pitch, S.svar.as<float>() + g0, pitch,
-                              (size_t)nb * 4, (size_t)S.k, hipMemcpyDeviceToHost, S.d2h));
+      if (bounce) {  // into slot bi % kSlots (drained kSlots - 1 batches later)
+        hipEvent_t dv;
+        const int dv_i = cev++;
+        HIPCHK(cevent(dv_i, &dv));
+        HIPCHK(hipMemcpy2DAsync(S.pin_out[bi % State::kSlots].p, (size_t)nb * 4,
+                                S.svar.as<float>() + g0, pitch, (size_t)nb * 4, (size_t)S.k,
+                                hipMemcpyDeviceToHost, S.d2h));
+        HIPCHK(hipEventRecord(dv, S.d2h));
+        d2h_done.push_back(dv_i);
+      } else {
+        HIPCHK(hipMemcpy2DAsync(sl->var + g0, pitch, S.svar.as<float>() + g0, pitch,
+                                (size_t)nb * 4, (size_t)S.k, hipMemcpyDeviceToHost, S.d2h));
+      }
+    }
+    if (bounce && piped) {  // host side while the GPU works: next batch in, batch bi - 2 out
+      if (bi + 1 < nbat)
+        if (int rc = bounce_fill(bi + 1)) return rc;
+      if (piped_back && bi >= State::kSlots - 1)
+        if (int rc = bounce_drain(bi - (State::kSlots - 1))) return rc;
     }
     search_ev.push_back({ev, ev + 1});
     solve_ev.push_back({ev + 2, ev + 3});
@@ -1026,12 +1263,17 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   hipEvent_t e_end, e_back;
   HIPCHK(event(ev, &e_end));
   HIPCHK(event(ev + 1, &e_back));
-  if (host && !piped_back)
+  if (host && !piped_back && !bounce)
     HIPCHK(hipMemcpyAsync(sl->var, S.svar.p, bvar, hipMemcpyDeviceToHost, S.stream));
   if (piped_back) {  // the call returns after the last batch's copy back
     HIPCHK(hipEventRecord(e_back, S.d2h));
     HIPCHK(hipStreamWaitEvent(S.stream, e_back, 0));
   }
+  if (bounce && piped_back)  // drain the last batches
+    for (long long bj = std::max<long long>(0, nbat - (State::kSlots - 1)); bj < nbat; ++bj)
+      if (int rc = bounce_drain(bj)) return rc;
+  if (bounce && !piped_back)  // the whole slab back (after tune_q, or a staggered slab)
+    if (int rc = bounce_whole(false)) return rc;
   HIPCHK(hipEventRecord(e_end, S.stream));
   DevStats ds;
   HIPCHK(hipMemcpyAsync(&ds, S.stats.p, sizeof ds, hipMemcpyDeviceToHost, S.stream));
@@ -1060,6 +1302,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   // copies: x, y, alt (+ var when not piped) before the batches, var back after the last
   // solve; piped transfers overlap the batches and are not counted here
   st.ms_copy = elapsed(1, 2) + (host && !piped_back ? elapsed(ev - 1, ev) : 0.0f);
+  if (bounce) st.ms_copy = g_bounce_ms;  // the host threads' bounce copies
   st.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
   if (stats) *stats = st;
   return CWBL_OK;

@@ -191,7 +191,8 @@ typedef struct cwbl_stats {
   double    ms_prep;         /* tree build + obs QC tables */
   double    ms_search;       /* neighbour search kernels */
   double    ms_solve;        /* solve kernels (+ the tune_q pass when requested) */
-  double    ms_copy;         /* host<->device copies of the slab (host memory only) */
+  double    ms_copy;         /* host<->device copies of the slab (host memory only; for a */
+                             /* pageable slab: host time in its page-locked bounce copies) */
 } cwbl_stats;
 
 int         cwbl_init(const cwbl_init_params *params);

@@ -892,25 +892,36 @@ def test_ingested_obs_set_analysis_vs_oracle():
 
 
 @pytest.mark.parametrize("tune_q", [0, 1])
-def test_pipelined_host_slab_equals_device_slab(tune_q, monkeypatch):
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("staggered", [False, True])
+def test_pipelined_host_slab_equals_device_slab(tune_q, pinned, staggered, monkeypatch):
     """A host-memory slab whose analysed region is the whole horizontal slab moves var batch
     by batch (H2D before each batch's solve on its own stream, D2H behind each batch's last
-    solve; with tune_q the copy back waits for the whole slab): bit-identical to the
-    device-memory call, over many batches."""
+    solve; with tune_q the copy back waits for the whole slab).  Pageable numpy arrays go
+    through the library's page-locked bounce slots (host threads fill and drain them),
+    page-locked ones (torch pin_memory) are copied directly.  A staggered slab (ix_lim < nx,
+    the U variable's Q2 bounds) moves whole.  Bit-identical to the device-memory call, over
+    many batches."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("CWBL_MAX_BATCH", "3000")
     _cores.clear()
     w = _radar_case_scaled(0.1, nz=12)
     vp = w.vp
     vp.tune_q = tune_q
+    ix_lim = w.x.shape[1] - 1 if staggered else None
     c = abi.Core(w.k, device=0)
     c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
-    hv = w.var.copy()
-    st = c.analyze_var(vp, abi.make_slab(w.x, w.y, w.alt, hv))
+    if pinned:
+        t = torch.empty(w.var.shape, dtype=torch.float32, pin_memory=True)
+        t.copy_(torch.from_numpy(w.var))
+        hv = t.numpy()
+    else:
+        hv = w.var.copy()
+    st = c.analyze_var(vp, abi.make_slab(w.x, w.y, w.alt, hv, ix_lim=ix_lim))
     dev = torch.device("cuda:0")
     x, y, alt, dv = (torch.from_numpy(np.ascontiguousarray(a)).to(dev)
                      for a in (w.x, w.y, w.alt, w.var.copy()))
-    c.analyze_var(vp, abi.make_slab(x, y, alt, dv, memory=abi.MEM_DEVICE))
+    c.analyze_var(vp, abi.make_slab(x, y, alt, dv, ix_lim=ix_lim, memory=abi.MEM_DEVICE))
     c.finalize()
     assert st.solved > 0
     np.testing.assert_array_equal(hv.view(np.uint32), dv.cpu().numpy().view(np.uint32))

@@ -104,3 +104,43 @@ def test_bench_refuses_a_rank_count_that_is_not_gpus():
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 2, r.stderr
     assert "--gpus 2 but WORLD_SIZE=1" in r.stderr
+
+
+def test_roofline_block_takes_the_dominant_kernel_and_its_algorithmic_flops():
+    """bench.py's roofline: the kernel with the largest summed HIP-event time, its part of
+    letkf_solve's algorithmic flops (syrk + Yb d for the assembly; the dsytd2 steps' 4 n^2
+    and 6k^2 for the reflector solve) over that time; F stays reference-equivalent detail."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    k, solved, nobs = 40, 1000, 216_000
+    # the steps of dsytd2 sum to ~4k^3/3
+    tri = bench._tri_flops(k, 0, k)
+    assert tri == sum(4 * n * n for n in range(1, k)) and abs(tri / (4 * k ** 3 / 3) - 1) < 0.05
+    kt = {"assemble_record_kernel<4>": {"launches": 2, "points": solved, "ms": 3.0},
+          "solve_tq40_kernel<40, 0>": {"launches": 2, "points": solved, "ms": 2.0},
+          "search_binned_kernel": {"launches": 2, "points": solved, "ms": 9.0}}
+    roof, per = bench.roofline_block(kt, k, solved, nobs, 5.0, "no-such-config")
+    assert roof["kernel"] == "assemble_record_kernel<4>"  # the search has no FP64 model
+    want = nobs * (k * (k + 1) + 2 * k) / 3e-3 / 1e12
+    assert abs(roof["achieved"] - want) < 1e-9 and roof["frac"] == roof["achieved"] / 78.6
+    assert roof["avg_launch_ms"] == 1.5 and "algorithmic_tflops" not in per["search_binned_kernel"]
+    tq = per["solve_tq40_kernel<40, 0>"]["algorithmic_tflops"]
+    assert abs(tq - solved * (tri + 6 * k * k) / 2e-3 / 1e12) < 1e-9
+    # the split k = 128 pair: steps 0..63 in the hand-off kernel, the rest in the tail
+    a = bench.kernel_algorithmic_flops("solve_tq_big_kernel<128, false, 64>", 128, 1, 200)
+    b = bench.kernel_algorithmic_flops("solve_tqb_tail_kernel<128, 64, 2>", 128, 1, 200)
+    assert a + b == 200 * (128 * 129 + 256) + bench._tri_flops(128, 0, 128) + 6 * 128 * 128
+
+
+def test_baseline_process_count_follows_affinity_and_quota():
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    n_aff, n_phys, quota = bench.host_cores()
+    assert 1 <= n_phys <= n_aff == len(os.sched_getaffinity(0))
+    procs, note = bench.baseline_procs()
+    assert procs == (n_phys if quota is None else max(1, min(n_phys, int(quota))))
+    assert f"{procs} used" in note
