@@ -233,10 +233,12 @@ struct State {
   DevBuf wsa;                                         // hand-off records (split KP=40 path)
   DevBuf flags;                                       // binned search: flagged points (+ count)
   bool binned = true;                                 // CWBL_SEARCH=tree: k-d tree search only
+  int bin_div = 2;                                    // CWBL_BIN_DIV: bin side = radius / bin_div
   bool jacobi = false;                                // CWBL_SOLVER=jacobi: eigen path
   int tq4 = 1;  // CWBL_TQ4: KP=40 solve 0 = one kernel, else assembly record + solve_tq40
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: record batch (points)
   bool big_split = true;                              // CWBL_BIG_SPLIT=0: one-kernel KP=128 solve
+  bool big_streams = false;  // CWBL_BIG_STREAMS=1: the split k > 64 path's tail on its own stream
   long long big_sub = 98304;                          // CWBL_BIG_SUB: KP=128 hand-off batch
   std::vector<hipEvent_t> events;
   hipStream_t h2d = nullptr, d2h = nullptr;           // host-memory slab copies (pipelined)
@@ -497,7 +499,7 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
       if (!h.ind.empty())
         HIPCHK(hipMemcpyAsync(nt->ind.p, h.ind.data(), h.ind.size() * sizeof(int),
                               hipMemcpyHostToDevice, S.stream));
-      build_bins(h, tdim, std::sqrt(search_r2()), nt->bins);
+      build_bins(h, tdim, std::sqrt(search_r2()), nt->bins, S.bin_div);
       const HostBins &hb = nt->bins;
       HIPCHK(nt->bxyz.ensure(hb.xyzs.size() * sizeof(float) + 16));
       HIPCHK(nt->bstart.ensure(hb.start.size() * sizeof(int)));
@@ -711,6 +713,10 @@ int cwbl_init(const cwbl_init_params *p) {
     S.binned = !(e && std::strcmp(e, "tree") == 0);
   }
   if (const char *e = std::getenv("CWBL_BIG_SPLIT")) S.big_split = std::atoi(e) != 0;
+  S.bin_div = 2;
+  if (const char *e = std::getenv("CWBL_BIN_DIV")) S.bin_div = std::max(1, std::min(8, std::atoi(e)));
+  S.big_streams = false;
+  if (const char *e = std::getenv("CWBL_BIG_STREAMS")) S.big_streams = std::atoi(e) != 0;
   if (const char *e = std::getenv("CWBL_BIG_SUB")) S.big_sub = std::max(64LL, std::atoll(e));
   if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
   S.serial_search = false;
@@ -1050,7 +1056,12 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   // busy, the four-point solve is latency-bound).  Two record and two info buffers; an
   // assembly waits for the solve two record batches back (record reuse) and for the info
   // reduction two search batches back (info reuse).
-  const bool conc = S.tq40_streams && S.tq4 && S.kp == kTq4KP && !S.jacobi;
+  const bool big_split_path = (S.kp == 96 || S.kp == kBigSplitKP) && S.big_split &&
+                              S.k > big_split_j0(S.kp) + 2;
+  // (the same two-stream scheme for the k > 64 split path: the one-wavefront tail of a
+  // hand-off sub-batch beside the next sub-batch's 256-thread kernel, CWBL_BIG_STREAMS)
+  const bool conc = (S.tq40_streams && S.tq4 && S.kp == kTq4KP && !S.jacobi) ||
+                    (S.big_streams && big_split_path);
   int nrec = 0;                 // record batches so far
   std::vector<int> rec_done;    // cevent after each record batch's solve (on S.tstream)
   std::vector<int> info_done;   // cevent after each search batch's info reduction
@@ -1108,7 +1119,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       HIPCHK(hipStreamWaitEvent(S.stream, hv, 0));
     }
     HIPCHK(hipEventRecord(b2, S.stream));
-    if ((S.kp == 96 || S.kp == kBigSplitKP) && S.big_split && S.k > big_split_j0(S.kp) + 2) {
+    if (big_split_path) {
       // 256-thread assembly + first kBigJ0 steps -> workspace -> one-wavefront tail, in
       // hand-off batches of Bs points (a multiple of kListLanes; BigHandoff<128, 64> is
       // 134.7 KB per point, 13 GB at the default 98 304, outside workspace_bytes)
@@ -1123,6 +1134,33 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       long long Bs = (nb + nsub - 1) / nsub;
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
       HIPCHK(S.wsa.ensure((size_t)Bs * rec_bytes));
+      if (conc) {  // two hand-off and two info buffers (see the record path below)
+        HIPCHK(S.wsa2.ensure((size_t)Bs * rec_bytes));
+        int2 *binfo = (bi & 1) ? S.info2.as<int2>() : S.info.as<int2>();
+        if (bi >= 2) HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[info_done[bi - 2]], 0));
+        for (long long s0 = 0; s0 < nb; s0 += Bs) {
+          const int ns = (int)std::min<long long>(Bs, nb - s0);
+          double *recp = (nrec & 1) ? S.wsa2.as<double>() : S.wsa.as<double>();
+          if (nrec >= 2)  // this hand-off buffer: finished by the tail two sub-batches back
+            HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[rec_done[nrec - 2]], 0));
+          HIPCHK(kt_begin(S.stream, &kt));
+          HIPCHK(launch_big_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,
+                                    nidx + s0 * list_cap, binfo + s0, recp));
+          HIPCHK(kt_end(S.stream, kt, KT_BIG_HANDOFF, ns));
+          hipEvent_t ea, et;
+          HIPCHK(cevent(cev, &ea));
+          HIPCHK(cevent(cev + 1, &et));
+          HIPCHK(hipEventRecord(ea, S.stream));
+          HIPCHK(hipStreamWaitEvent(S.tstream, ea, 0));
+          HIPCHK(kt_begin(S.tstream, &kt));
+          HIPCHK(launch_solve_tqb_tail(S.tstream, S.kp, c, sd, g0 + s0, ns, recp, binfo + s0));
+          HIPCHK(kt_end(S.tstream, kt, KT_TQB_TAIL, ns));
+          HIPCHK(hipEventRecord(et, S.tstream));
+          rec_done.push_back(cev + 1);
+          cev += 2;
+          ++nrec;
+        }
+      } else
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
         const int ns = (int)std::min<long long>(Bs, nb - s0);
         HIPCHK(kt_begin(S.stream, &kt));

@@ -72,7 +72,7 @@ struct HostBins {
 };
 // Bins of side ~r/2 (r: the search radius in normalised units) over a built tree's
 // rearranged coordinates; dim 2 ignores z.  Capped at 2^22 cells.
-void build_bins(const HostTree &t, int dim, float r, HostBins &out);
+void build_bins(const HostTree &t, int dim, float r, HostBins &out, int div = 2);
 
 // Per-variable constants of the solve.
 struct SolveConsts {

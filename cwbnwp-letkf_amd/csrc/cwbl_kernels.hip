@@ -307,53 +307,31 @@ hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int d
 // search_binned_kernel: one lane per grid point.  The fixed-radius sets of search_kernel
 // (same normalisation, the same fp32 distance d - q in dimension order and d2 <= r2 test as
 // process_terminal_node_fixedball, module_kdtree2.f90:1654-1707) from uniform bins: the
-// cells of the ball's bounding box are, per (iy, iz), one contiguous run of points.  The sets
-// are identical; the order is the bins', which only changes the order of the fp64 sums of the
-// solve.  Where kdtree2's order decides WHICH points are kept (a list past max_lz, Q4) the
-// point is flagged and search_kernel<FlagQuery> redoes it.
-//
-// r4: the wave scans its lanes' runs together.  Per (iz, iy) row of cells of the union of the
-// lanes' boxes, the run is the union of the lanes' x-trimmed runs; each chunk of 64 of its
-// points is loaded once (one coalesced load per lane) and broadcast lane by lane
-// (v_readlane), and every lane tests every point of the chunk against its own query.  A
-// point outside a lane's own run is outside its ball (the runs are conservative), so it
-// fails that lane's d2 <= r2 test, and a lane meets its own points in the same (iz, iy, x)
-// order as a scan of its own runs: the lists, counts and overflow flags are those of the
-// per-lane scan, while the loads drop from one per lane and candidate to one per wave and
-// 64 candidates.  (The per-lane scan was bound by those loads: at C5, ~2 600 16-B candidate
-// loads per point from the MALL, 2.2 ms per 133 k-point batch.)
+// cells of the ball's bounding box are, per (iy, iz), one contiguous run of points, so a
+// lane streams through at most 5 x 5 runs instead of walking the tree (divergent, latency
+// bound).  The sets are identical; the order is the bins', which only changes the order of
+// the fp64 sums of the solve.  Where kdtree2's order decides WHICH points are kept (a list
+// past max_lz, Q4) the point is flagged and search_kernel<FlagQuery> redoes it.
 // ---------------------------------------------------------------------------------------
-__device__ inline int wave_min_i(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ inline int wave_max_i(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ inline float bcast_f(float v, int lane) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
-
+constexpr int kBinAhead = 8;  // bin points loaded ahead of their tests
 __global__ void __launch_bounds__(64)
 search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, float r2,
                      float rbox, SlabQuery qs, int npts, int *__restrict__ nbr_cnt,
                      int *__restrict__ nbr_idx, int *__restrict__ flag_cnt,
                      int *__restrict__ flag_idx) {
-  const int lane = threadIdx.x;
-  const int gi = blockIdx.x * 64 + lane;
-  const bool live = gi < npts;
-  float px = 0.0f, py = 0.0f, pz = 0.0f;
-  if (live) qs.at(gi, px, py, pz);
+  // (XCD-aware block order, r4: consecutive blocks of an XCD take consecutive 64-point runs
+  // of the row, whose candidate cells overlap, so an XCD's L2 serves its neighbours' loads;
+  // with round-robin dealing each XCD saw every eighth run)
+  const int gi = xcd_remap(blockIdx.x, gridDim.x) * 64 + threadIdx.x;
+  if (gi >= npts) return;
+  float px, py, pz;
+  qs.at(gi, px, py, pz);
   bool flagged = false;
-  constexpr int kNone = 0x3fffffff;
   for (int t = 0; t < ntrees; ++t) {
     const TreeDesc &T = trees[t];
     const float q0 = px * T.hclr_inv, q1 = py * T.hclr_inv;  // get_lz (:243-253)
     const float q2 = T.query3d ? pz * T.vclr_inv : 0.0f;
-    int *__restrict__ out = nbr_idx + list_index(live ? gi : 0, list_cap, T.list_off);
+    int *__restrict__ out = nbr_idx + list_index(gi, list_cap, T.list_off);
     const int dim = T.tree_dim, max_lz = T.max_lz;
     int count = 0;
     bool ovf = false;
@@ -373,10 +351,7 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
       crange(q0, T.bx0, T.nbx, ix0, ix1);
       crange(q1, T.by0, T.nby, iy0, iy1);
       if (dim == 3) crange(q2, T.bz0, T.nbz, iz0, iz1);
-      if (ix0 > ix1 || !live) {  // the box misses the grid in x (or no point): no rows
-        iy0 = kNone;
-        iy1 = -1;
-      }
+      if (ix0 > ix1) iy1 = iy0 - 1;  // the box misses the grid in x
       // distance from q to the slab of cell row/layer i along one axis, shrunk by a margin
       // (conservative against the fp32 cell assignment)
       const float h = 1.0f / T.binv, rb2 = rbox * rbox;
@@ -385,46 +360,39 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
         const float g = fmaxf(fmaxf(lo - q, q - hi), 0.0f);
         return fmaxf(g - 1e-3f * h - margin(q, b0), 0.0f);
       };
-      const bool rows = iy0 <= iy1;
-      const int uy0 = wave_min_i(rows ? iy0 : kNone), uy1 = wave_max_i(rows ? iy1 : -1);
-      const int uz0 = wave_min_i(rows ? iz0 : kNone), uz1 = wave_max_i(rows ? iz1 : -1);
-      for (int iz = uz0; iz <= uz1; ++iz) {
+      for (int iz = iz0; iz <= iz1 && !ovf; ++iz) {
         const float gz = dim == 3 ? gap(q2, T.bz0, iz) : 0.0f;
-        for (int iy = uy0; iy <= uy1; ++iy) {
-          // this lane's run of the row: the ball's x-extent over it
-          int jx0 = kNone, jx1 = -1;
-          if (rows && iy >= iy0 && iy <= iy1 && iz >= iz0 && iz <= iz1) {
-            const float gy = gap(q1, T.by0, iy);
-            const float rem = rb2 - gy * gy - gz * gz;
-            if (rem >= 0.0f) {
-              const float xh = sqrtf(rem) + margin(q0, T.bx0);
-              jx0 = max(ix0, (int)fminf(fmaxf(floorf((q0 - xh - T.bx0) * T.binv), 0.0f),
-                                        (float)T.nbx));
-              jx1 = min(ix1, (int)fminf(fmaxf(floorf((q0 + xh - T.bx0) * T.binv), -1.0f),
-                                        (float)(T.nbx - 1)));
-            }
-          }
-          const int ux0 = wave_min_i(jx0 <= jx1 ? jx0 : kNone);
-          const int ux1 = wave_max_i(jx0 <= jx1 ? jx1 : -1);
-          if (ux0 > ux1) continue;
+        for (int iy = iy0; iy <= iy1 && !ovf; ++iy) {
+          // the ball's x-extent over this row of cells
+          const float gy = gap(q1, T.by0, iy);
+          const float rem = rb2 - gy * gy - gz * gz;
+          if (rem < 0.0f) continue;
+          const float xh = sqrtf(rem) + margin(q0, T.bx0);
+          const int jx0 = max(ix0, (int)fminf(fmaxf(floorf((q0 - xh - T.bx0) * T.binv), 0.0f),
+                                               (float)T.nbx));
+          const int jx1 = min(ix1, (int)fminf(fmaxf(floorf((q0 + xh - T.bx0) * T.binv), -1.0f),
+                                               (float)(T.nbx - 1)));
+          if (jx0 > jx1) continue;
           const int cb = (iz * T.nby + iy) * T.nbx;
-          const int e = T.bstart[cb + ux1 + 1];
-          for (int i0 = T.bstart[cb + ux0]; i0 < e; i0 += 64) {
-            const int n = min(64, e - i0);
-            const float4 mine = T.bxyz[min(i0 + lane, e - 1)];
-            for (int c = 0; c < n; ++c) {
-              const float dx = bcast_f(mine.x, c) - q0, dy = bcast_f(mine.y, c) - q1;
+          const int e = T.bstart[cb + jx1 + 1];
+          for (int i0 = T.bstart[cb + jx0]; i0 < e; i0 += kBinAhead) {
+            float4 d[kBinAhead];
+#pragma unroll
+            for (int a = 0; a < kBinAhead; ++a) d[a] = T.bxyz[min(i0 + a, e - 1)];
+#pragma unroll
+            for (int a = 0; a < kBinAhead; ++a) {
+              const float dx = d[a].x - q0, dy = d[a].y - q1;
               float sd = dx * dx;
               sd = sd + dy * dy;
               if (dim == 3) {
-                const float dz = bcast_f(mine.z, c) - q2;
+                const float dz = d[a].z - q2;
                 sd = sd + dz * dz;
               }
-              const int slot = __builtin_amdgcn_readlane(__float_as_int(mine.w), c);
-              if (sd <= r2 && !ovf && live) {
+              if (i0 + a < e && sd <= r2 && !ovf) {
                 if (count == max_lz) {
                   ovf = true;
                 } else {
+                  const int slot = __float_as_int(d[a].w);
                   const int g = count % kListGroup;
                   grp.x = g == 0 ? slot : grp.x;
                   grp.y = g == 1 ? slot : grp.y;
@@ -436,13 +404,14 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
                 }
               }
             }
+            if (ovf) break;
           }
         }
       }
-      if (live && count % kListGroup != 0)
+      if (count % kListGroup != 0)
         *reinterpret_cast<int4 *>(out + list_slot(count - count % kListGroup)) = grp;
     }
-    if (live) nbr_cnt[(long long)gi * ntrees + t] = count;
+    nbr_cnt[(long long)gi * ntrees + t] = count;
     flagged = flagged || ovf;
   }
   if (flagged) flag_idx[atomicAdd(flag_cnt, 1)] = gi;

@@ -378,12 +378,6 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     // The previous full step read col only before its four later barriers, so only the
     // step after the (barrier-free) trailing step k-2 needs one here.
     if (j >= k - 1) __syncthreads();
-    // x'_{j+1}, b1_{j+1} for every thread's v.x', v.b1 (read after the next barrier; the last
-    // readers, the previous step's, are behind its later barriers)
-    if (tid == j + 1) {
-      sm.piv[0] = ux;
-      sm.piv[1] = ub;
-    }
     CWBL_PUBLISH(j, sm.col);
     __syncthreads();
     const double dj = sm.col[j];
@@ -414,28 +408,19 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     // are skipped below, and the row sums rely on every block's last live step
     // (j = 4 bj + 3, where v vanishes on its columns) leaving exact zeros in its A v partials.
     const double v = tid == j + 1 ? 1.0 : x * scal;
-    // v for the update, read after bsum1's barrier.  The matvec needs no barrier for it: a
-    // thread forms the v entries of its blocks from the published column itself (v_r =
-    // col_r scal past row j+1, 1 at j+1, 0 above; rows >= k hold exact zeros in col), one
-    // barrier per step fewer.
     if (tid < KP) sm.vb[tid] = v;
-    auto vload = [&](int r0, double (&o)[4]) {
-      ld4(&sm.col[r0], o);
-      if (r0 > j + 1) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] *= scal;
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = r0 + q > j + 1 ? o[q] * scal : r0 + q == j + 1 ? 1.0 : 0.0;
-      }
-    };
+    if (tid == j + 1) {  // x'_{j+1}, b1_{j+1} for every thread's v.x', v.b1
+      sm.piv[0] = ux;
+      sm.piv[1] = ub;
+    }
+    __syncthreads();
     double s1p = 0.0;
 #pragma unroll
     for (int it = 0; it < NBL; ++it) {
       if (tid + NT * it < NBLK && bj[it] >= J) {
         double vi[4], vj[4];
-        vload(4 * bi[it], vi);
-        vload(4 * bj[it], vj);
+        ld4(&sm.vb[4 * bi[it]], vi);
+        ld4(&sm.vb[4 * bj[it]], vj);
         double pr[4], pc[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -475,15 +460,12 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     if (tid < KP && tid > j) {
       const double *prow = &sm.u.pb[tid >> 2][tid & 3];
       // block columns < J hold exact zeros (dead blocks): start at the 8-column segment of J
-      // (four chains: the sequential sum's 32 dependent adds were the longest latency chain
-      // of the step, run by waves 0-1 alone while waves 2-3 wait at the next barrier)
       auto rsum = [&](auto C) {
         constexpr int c0 = decltype(C)::value;
-        static_assert((SM::NB - c0) % 4 == 0, "row-sum chains");
-        double t[4] = {0.0, 0.0, 0.0, 0.0};
+        double t = 0.0;
 #pragma unroll
-        for (int cb = c0; cb < SM::NB; ++cb) t[(cb - c0) & 3] += prow[4 * cb];
-        return (t[0] + t[1]) + (t[2] + t[3]);
+        for (int cb = c0; cb < SM::NB; ++cb) t += prow[4 * cb];
+        return t;
       };
       const int seg = J >> 3;
       if (seg >= 3 && SM::NB > 24) pp = rsum(std::integral_constant<int, (SM::NB > 24 ? 24 : 0)>{});

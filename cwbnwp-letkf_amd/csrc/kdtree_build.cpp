@@ -118,7 +118,7 @@ void build_kdtree(const float *xyz3, int n, int dim, HostTree &out) {
       out.rdata[4 * static_cast<size_t>(i) + d] = d < dim ? xyz3[3 * out.ind[i] + d] : 0.0f;
 }
 
-void build_bins(const HostTree &t, int dim, float r, HostBins &out) {
+void build_bins(const HostTree &t, int dim, float r, HostBins &out, int div) {
   const int n = t.n;
   out = HostBins{};
   // bounds over the finite coordinates (a non-finite point is never within r: d2 <= r2 fails
@@ -134,7 +134,7 @@ void build_bins(const HostTree &t, int dim, float r, HostBins &out) {
       seen[c] = true;
     }
   if (dim < 3) lo[2] = hi[2] = 0.0f;
-  float h = 0.5f * r;
+  float h = r / (float)std::max(div, 1);  // cell side r / div (div 2: the ball's box spans ~5 cells)
   long long nb[3];
   for (;;) {
     for (int c = 0; c < 3; ++c)

@@ -6,7 +6,7 @@ mkdir -p gpurun_out/ab
 for rep in $(seq 1 ${REPS:-3}); do
   for L in $LIBS; do
     tag=$(basename $L)
-    CWBL_LIBRARY=$PWD/$L/libcwbl.so timeout -k 10 120 python3 bench.py --steps 6 --warmup 2 \
+    CWBL_LIBRARY=$PWD/$L/libcwbl.so timeout -k 10 120 python3 bench.py --steps ${STEPS:-6} --warmup ${WARMUP:-2} \
       --no-cpu-baseline --no-cycle --no-detail-configs $BENCH_ARGS > gpurun_out/ab/$tag.$rep.log 2>&1 || { tail -5 gpurun_out/ab/$tag.$rep.log; exit 5; }
     python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], 'rep', sys.argv[3], round(d['value']/1e6,2), 'M', round(d['ms_per_step'],2), 'ms')" gpurun_out/ab/$tag.$rep.log $tag $rep
   done
