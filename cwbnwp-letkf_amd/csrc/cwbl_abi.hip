@@ -233,7 +233,8 @@ struct State {
   DevBuf wsa;                                         // hand-off records (split KP=40 path)
   DevBuf flags;                                       // binned search: flagged points (+ count)
   bool binned = true;                                 // CWBL_SEARCH=tree: k-d tree search only
-  int bin_div = 2;                                    // CWBL_BIN_DIV: bin side = radius / bin_div
+  int bin_div = 0;  // CWBL_BIN_DIV: bin side = radius / bin_div (0: by density, bin_div_for)
+  bool pageable_register = true;                      // CWBL_PAGEABLE=bounce: bounce slots
   bool jacobi = false;                                // CWBL_SOLVER=jacobi: eigen path
   int tq4 = 1;  // CWBL_TQ4: KP=40 solve 0 = one kernel, else assembly record + solve_tq40
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: record batch (points)
@@ -440,6 +441,31 @@ hipError_t order_after_caller() {
   return hipStreamWaitEvent(S.stream, S.order_ev, 0);
 }
 
+// Bin side r / div for the uniform-bin search: r/2 by default; r/4 where the obs are dense
+// (more than 24 per r/2 cell on average over the set's bounding box: the finer cells trim
+// the per-row runs closer to the ball).  r4 A/B: C5 (49 per r/2 cell) 15.95 M pts/s at r/2,
+// 16.04 at r/3, 16.19 at r/4; C2 (~11 per cell) 59.4 / 58.9 / 58.6.  CWBL_BIN_DIV forces it.
+int bin_div_for(const HostTree &t, int dim) {
+  if (S.bin_div > 0) return S.bin_div;
+  const int n = t.n;
+  if (n == 0) return 2;
+  float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+  bool seen = false;
+  for (int i = 0; i < n; ++i) {
+    const float *d = &t.rdata[4 * (size_t)i];
+    if (!std::isfinite(d[0]) || !std::isfinite(d[1]) || (dim == 3 && !std::isfinite(d[2]))) continue;
+    for (int c = 0; c < dim; ++c) {
+      lo[c] = seen ? std::min(lo[c], d[c]) : d[c];
+      hi[c] = seen ? std::max(hi[c], d[c]) : d[c];
+    }
+    seen = true;
+  }
+  const double h = 0.5 * std::sqrt((double)search_r2());
+  double cells = 1.0;
+  for (int c = 0; c < dim; ++c) cells *= std::max(1.0, ((double)hi[c] - (double)lo[c]) / h);
+  return (double)n / cells > 24.0 ? 4 : 2;
+}
+
 // Builds the trees of one family (build_tree, module_localization.f90:35-167) and their
 // column tables.  Appends TreeDesc entries.
 int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &descs,
@@ -499,7 +525,7 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
       if (!h.ind.empty())
         HIPCHK(hipMemcpyAsync(nt->ind.p, h.ind.data(), h.ind.size() * sizeof(int),
                               hipMemcpyHostToDevice, S.stream));
-      build_bins(h, tdim, std::sqrt(search_r2()), nt->bins, S.bin_div);
+      build_bins(h, tdim, std::sqrt(search_r2()), nt->bins, bin_div_for(h, tdim));
       const HostBins &hb = nt->bins;
       HIPCHK(nt->bxyz.ensure(hb.xyzs.size() * sizeof(float) + 16));
       HIPCHK(nt->bstart.ensure(hb.start.size() * sizeof(int)));
@@ -713,7 +739,9 @@ int cwbl_init(const cwbl_init_params *p) {
     S.binned = !(e && std::strcmp(e, "tree") == 0);
   }
   if (const char *e = std::getenv("CWBL_BIG_SPLIT")) S.big_split = std::atoi(e) != 0;
-  S.bin_div = 2;
+  S.pageable_register = true;
+  if (const char *e = std::getenv("CWBL_PAGEABLE")) S.pageable_register = std::strcmp(e, "bounce") != 0;
+  S.bin_div = 0;  // 0: by density (bin_div_for)
   if (const char *e = std::getenv("CWBL_BIN_DIV")) S.bin_div = std::max(1, std::min(8, std::atoi(e)));
   S.big_streams = false;
   if (const char *e = std::getenv("CWBL_BIG_STREAMS")) S.big_streams = std::atoi(e) != 0;
@@ -909,7 +937,25 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   // pageable var (a Fortran host's ordinary arrays): copies from pageable memory are staged
   // by the runtime and do not overlap, so var goes through the library's page-locked bounce
   // slots instead, filled / drained by host threads while the GPU runs other batches
-  const bool bounce = host && bvar > 0 && !host_pinned(sl->var);
+  bool bounce = host && bvar > 0 && !host_pinned(sl->var);
+  // A pageable var is page-locked in place for the call (hipHostRegister, undone on return)
+  // and then copied like page-locked memory: r4, C2 from pageable numpy arrays 58.7 M pts/s
+  // against 58.2 M from page-locked ones and 50.8 M through the bounce slots, whose host
+  // copies stall the pipeline.  The slots remain the fallback when the registration fails
+  // (and CWBL_PAGEABLE=bounce forces them).
+  bool registered = false;
+  if (bounce && S.pageable_register) {
+    if (hipHostRegister(sl->var, bvar, hipHostRegisterDefault) == hipSuccess) {
+      registered = true;
+      bounce = false;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
+  struct Unregister {  // on every return path
+    bool on; void *p;
+    ~Unregister() { if (on) (void)hipHostUnregister(p); }
+  } unreg{registered, sl->var};
   if (!host) {
     sd.x = sl->x; sd.y = sl->y; sd.alt = sl->alt; sd.var = sl->var;
   } else {

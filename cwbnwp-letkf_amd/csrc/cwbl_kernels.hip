@@ -319,10 +319,9 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
                      float rbox, SlabQuery qs, int npts, int *__restrict__ nbr_cnt,
                      int *__restrict__ nbr_idx, int *__restrict__ flag_cnt,
                      int *__restrict__ flag_idx) {
-  // (XCD-aware block order, r4: consecutive blocks of an XCD take consecutive 64-point runs
-  // of the row, whose candidate cells overlap, so an XCD's L2 serves its neighbours' loads;
-  // with round-robin dealing each XCD saw every eighth run)
-  const int gi = xcd_remap(blockIdx.x, gridDim.x) * 64 + threadIdx.x;
+  // (r4: an XCD-aware block order, consecutive 64-point runs on one XCD, measured a tie at C2
+  // and C5 against this round-robin one)
+  const int gi = blockIdx.x * 64 + threadIdx.x;
   if (gi >= npts) return;
   float px, py, pz;
   qs.at(gi, px, py, pz);

@@ -9,3 +9,4 @@ LIBS="_ab/oldsearch _ab/xcd" REPS=2 STEPS=2 WARMUP=1 BENCH_ARGS="--config c5 --n
 ENVS="CWBL_BIN_DIV=2 CWBL_BIN_DIV=3 CWBL_BIN_DIV=4" CFG=c5 REPS=1 STEPS=2 timeout -k 10 400 bash scripts/ab_env.sh 2>&1 | tee $O/bindiv_c5.txt
 ENVS="CWBL_BIN_DIV=2 CWBL_BIN_DIV=3 CWBL_BIN_DIV=4" CFG=c2 REPS=1 STEPS=4 timeout -k 10 300 bash scripts/ab_env.sh 2>&1 | tee $O/bindiv_c2.txt
 for T in 16 8 4; do OMP_NUM_THREADS=$T timeout -k 10 200 python3 scripts/host_memory_ab.py 3 2>&1 | tee -a $O/host_ab.txt; done
+CWBL_PAGEABLE=register timeout -k 10 200 python3 scripts/host_memory_ab.py 3 2>&1 | sed 's/^/register: /' | tee -a $O/host_ab.txt

@@ -892,18 +892,22 @@ def test_ingested_obs_set_analysis_vs_oracle():
 
 
 @pytest.mark.parametrize("tune_q", [0, 1])
-@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("host", ["pageable", "pageable_bounce", "pinned"])
 @pytest.mark.parametrize("staggered", [False, True])
-def test_pipelined_host_slab_equals_device_slab(tune_q, pinned, staggered, monkeypatch):
+def test_pipelined_host_slab_equals_device_slab(tune_q, host, staggered, monkeypatch):
     """A host-memory slab whose analysed region is the whole horizontal slab moves var batch
     by batch (H2D before each batch's solve on its own stream, D2H behind each batch's last
-    solve; with tune_q the copy back waits for the whole slab).  Pageable numpy arrays go
-    through the library's page-locked bounce slots (host threads fill and drain them),
+    solve; with tune_q the copy back waits for the whole slab).  Pageable numpy arrays are
+    page-locked in place for the call (hipHostRegister) or, with CWBL_PAGEABLE=bounce, go
+    through the library's page-locked bounce slots (host threads fill and drain them);
     page-locked ones (torch pin_memory) are copied directly.  A staggered slab (ix_lim < nx,
     the U variable's Q2 bounds) moves whole.  Bit-identical to the device-memory call, over
     many batches."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("CWBL_MAX_BATCH", "3000")
+    if host == "pageable_bounce":
+        monkeypatch.setenv("CWBL_PAGEABLE", "bounce")
+    pinned = host == "pinned"
     _cores.clear()
     w = _radar_case_scaled(0.1, nz=12)
     vp = w.vp
