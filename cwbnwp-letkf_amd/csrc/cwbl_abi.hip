@@ -706,16 +706,8 @@ int cwbl_init(const cwbl_init_params *p) {
     HIPCHK(hipMemGetInfo(&fr, &tot));
     S.handoff_budget = std::min<size_t>((size_t)13 << 30, fr / 10 * 4);
   }
-  {
-    const char *e = std::getenv("CWBL_SSTREAM_PRIO");
-    const int mode = e ? std::atoi(e) : 0;
-    int least = 0, greatest = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HIPCHK(hipStreamCreateWithPriority(&S.stream, hipStreamNonBlocking,
-                                       (mode & 2) ? greatest : 0));
-    HIPCHK(hipStreamCreateWithPriority(&S.sstream, hipStreamNonBlocking,
-                                       (mode & 1) ? least : 0));
-  }
+  HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&S.sstream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.tstream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.h2d, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.d2h, hipStreamNonBlocking));

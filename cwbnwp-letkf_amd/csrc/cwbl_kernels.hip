@@ -319,8 +319,9 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
                      float rbox, SlabQuery qs, int npts, int *__restrict__ nbr_cnt,
                      int *__restrict__ nbr_idx, int *__restrict__ flag_cnt,
                      int *__restrict__ flag_idx) {
-  // (r4: an XCD-aware block order, consecutive 64-point runs on one XCD, measured a tie at C2
-  // and C5 against this round-robin one)
+  // (r4, measured and dropped: an XCD-aware block order, a tie at C2 and C5; four lanes per
+  // point, which cuts this kernel's time by 25% at C2 and 38% at C5 but, overlapped with the
+  // assembly, costs the step 1-2% at C2 through its extra issue cycles: profiles/r4k_*)
   const int gi = blockIdx.x * 64 + threadIdx.x;
   if (gi >= npts) return;
   float px, py, pz;
@@ -416,147 +417,13 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
   if (flagged) flag_idx[atomicAdd(flag_cnt, 1)] = gi;
 }
 
-// search_binned_quad_kernel: the same lists, slot for slot, as search_binned_kernel, with four
-// lanes per point.  One lane per point leaves a C5 batch (133 k points) with ~2 k waves whose
-// ~80 cell rows and ~2 500 candidates each are a chain of dependent global loads (bstart, then
-// the run): the search is latency bound.  Here a quad walks its point's cell rows four at a time
-// (lane r finds row 4 g + r's run), concatenates the four runs into one candidate stream in row
-// order, and tests it 32 candidates per round (lane r takes stream positions 8 r .. 8 r + 7 of
-// the round); a quad prefix sum of the accepted counts places every lane's slots, so the list
-// is the serial scan's.  Overflow (Q4) is the serial rule too: the point is flagged as soon as
-// the accepted count would pass max_lz, and search_kernel<FlagQuery> redoes it.
-constexpr int kQuadPer = 8;  // stream positions per lane and round
-__global__ void __launch_bounds__(64)
-search_binned_quad_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, float r2,
-                          float rbox, SlabQuery qs, int npts, int *__restrict__ nbr_cnt,
-                          int *__restrict__ nbr_idx, int *__restrict__ flag_cnt,
-                          int *__restrict__ flag_idx) {
-  const int lane = threadIdx.x, r = lane & 3, q0l = lane & ~3;
-  const int gi = blockIdx.x * 16 + (lane >> 2);
-  if (gi >= npts) return;  // quad-uniform
-  auto qget = [&](int v, int i) { return __shfl(v, q0l + i, 64); };
-  float px, py, pz;
-  qs.at(gi, px, py, pz);
-  bool flagged = false;
-  for (int t = 0; t < ntrees; ++t) {
-    const TreeDesc &T = trees[t];
-    const float q0 = px * T.hclr_inv, q1 = py * T.hclr_inv;  // get_lz (:243-253)
-    const float q2 = T.query3d ? pz * T.vclr_inv : 0.0f;
-    int *__restrict__ out = nbr_idx + list_index(gi, list_cap, T.list_off);
-    const int dim = T.tree_dim, max_lz = T.max_lz;
-    int count = 0;
-    bool ovf = false;
-    if (max_lz > 0) {
-      // the cell arithmetic of search_binned_kernel, unchanged
-      auto margin = [&](float q, float b0) { return 2e-6f * (fabsf(q) + fabsf(b0)); };
-      auto crange = [&](float q, float b0, int nb, int &a, int &b) {
-        const float rq = rbox + margin(q, b0);
-        const float lo = (q - rq - b0) * T.binv, hi = (q + rq - b0) * T.binv;
-        a = (int)fminf(fmaxf(floorf(lo), 0.0f), (float)nb);
-        b = (int)fminf(fmaxf(floorf(hi), -1.0f), (float)(nb - 1));
-      };
-      int ix0, ix1, iy0, iy1, iz0 = 0, iz1 = 0;
-      crange(q0, T.bx0, T.nbx, ix0, ix1);
-      crange(q1, T.by0, T.nby, iy0, iy1);
-      if (dim == 3) crange(q2, T.bz0, T.nbz, iz0, iz1);
-      if (ix0 > ix1) iy1 = iy0 - 1;  // the box misses the grid in x
-      const float h = 1.0f / T.binv, rb2 = rbox * rbox;
-      auto gap = [&](float q, float b0, int i) {
-        const float lo = b0 + (float)i * h, hi = lo + h;
-        const float g = fmaxf(fmaxf(lo - q, q - hi), 0.0f);
-        return fmaxf(g - 1e-3f * h - margin(q, b0), 0.0f);
-      };
-      const int nyr = max(iy1 - iy0 + 1, 0), nrows = nyr * max(iz1 - iz0 + 1, 0);
-      for (int rg = 0; rg < nrows && !ovf; rg += 4) {
-        // this lane's row (iz outer, iy inner: the serial order) and its run
-        int s = 0, len = 0;
-        const int row = rg + r;
-        if (row < nrows) {
-          const int iz = iz0 + row / nyr, iy = iy0 + row % nyr;
-          const float gz = dim == 3 ? gap(q2, T.bz0, iz) : 0.0f;
-          const float gy = gap(q1, T.by0, iy);
-          const float rem = rb2 - gy * gy - gz * gz;
-          if (rem >= 0.0f) {
-            const float xh = sqrtf(rem) + margin(q0, T.bx0);
-            const int jx0 = max(ix0, (int)fminf(fmaxf(floorf((q0 - xh - T.bx0) * T.binv), 0.0f),
-                                                (float)T.nbx));
-            const int jx1 = min(ix1, (int)fminf(fmaxf(floorf((q0 + xh - T.bx0) * T.binv), -1.0f),
-                                                (float)(T.nbx - 1)));
-            if (jx0 <= jx1) {
-              const int cb = (iz * T.nby + iy) * T.nbx;
-              s = T.bstart[cb + jx0];
-              len = T.bstart[cb + jx1 + 1] - s;
-            }
-          }
-        }
-        // the four runs as one stream: run i covers stream positions c_i .. c_{i+1} - 1
-        const int s0 = qget(s, 0), s1 = qget(s, 1), s2 = qget(s, 2), s3 = qget(s, 3);
-        const int c1 = qget(len, 0), c2 = c1 + qget(len, 1), c3 = c2 + qget(len, 2);
-        const int tot = c3 + qget(len, 3);
-        for (int base = 0; base < tot && !ovf; base += 4 * kQuadPer) {
-          const int p0 = base + kQuadPer * r;
-          float4 d[kQuadPer];
-#pragma unroll
-          for (int a = 0; a < kQuadPer; ++a) {
-            const int p = min(p0 + a, tot - 1);
-            const int idx = p < c1 ? s0 + p : p < c2 ? s1 + (p - c1) : p < c3 ? s2 + (p - c2)
-                                                                            : s3 + (p - c3);
-            d[a] = T.bxyz[idx];
-          }
-          unsigned acc = 0u;
-#pragma unroll
-          for (int a = 0; a < kQuadPer; ++a) {
-            const float dx = d[a].x - q0, dy = d[a].y - q1;
-            float sd = dx * dx;
-            sd = sd + dy * dy;
-            if (dim == 3) {
-              const float dz = d[a].z - q2;
-              sd = sd + dz * dz;
-            }
-            if (p0 + a < tot && sd <= r2) acc |= 1u << a;
-          }
-          const int n = __popc(acc);
-          const int n0 = qget(n, 0), n1 = qget(n, 1), n2 = qget(n, 2), n3 = qget(n, 3);
-          const int off = (r > 0 ? n0 : 0) + (r > 1 ? n1 : 0) + (r > 2 ? n2 : 0);
-          const int nround = n0 + n1 + n2 + n3;
-          if (count + nround > max_lz) {  // the serial scan would overflow in this round
-            ovf = true;
-            count = max_lz;
-            break;
-          }
-          int pos = count + off;
-#pragma unroll
-          for (int a = 0; a < kQuadPer; ++a) {
-            if (acc & (1u << a)) {
-              out[list_slot(pos)] = __float_as_int(d[a].w);
-              ++pos;
-            }
-          }
-          count += nround;
-        }
-      }
-    }
-    if (r == 0) nbr_cnt[(long long)gi * ntrees + t] = count;
-    flagged = flagged || ovf;
-  }
-  if (flagged && r == 0) flag_idx[atomicAdd(flag_cnt, 1)] = gi;
-}
-
 hipError_t launch_search_binned(hipStream_t s, const TreeDesc *trees, int ntrees, int list_cap,
                                 float r2, float rbox, SlabDev slab, long long g0, int npts,
                                 int *nbr_cnt, int *nbr_idx, int *flag_cnt, int *flag_idx) {
   if (npts <= 0) return hipSuccess;
   SlabQuery q{slab, g0};
-  static const bool lane_form = [] {
-    const char *e = getenv("CWBL_SEARCH_LANE");
-    return e && atoi(e) != 0;
-  }();
-  if (lane_form)
-    hipLaunchKernelGGL(search_binned_kernel, dim3((npts + 63) / 64), dim3(64), 0, s, trees,
-                       ntrees, list_cap, r2, rbox, q, npts, nbr_cnt, nbr_idx, flag_cnt, flag_idx);
-  else
-    hipLaunchKernelGGL(search_binned_quad_kernel, dim3((npts + 15) / 16), dim3(64), 0, s, trees,
-                       ntrees, list_cap, r2, rbox, q, npts, nbr_cnt, nbr_idx, flag_cnt, flag_idx);
+  hipLaunchKernelGGL(search_binned_kernel, dim3((npts + 63) / 64), dim3(64), 0, s, trees,
+                     ntrees, list_cap, r2, rbox, q, npts, nbr_cnt, nbr_idx, flag_cnt, flag_idx);
   return hipGetLastError();
 }
 
