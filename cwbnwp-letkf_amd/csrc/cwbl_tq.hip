@@ -658,7 +658,10 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
 //                                    b1(32..39) and the diagonals A(0,0), A(16,16) that the
 //                                    yo rows of T0 and T2 displaced
 // = 3 x 64 + 5 x 16 = 272 matrix-pipe cycles per 4 columns for the 860 needed entries (215
-// cycles of work; 1.27x), against 336 for the 48 x 48 tiling with a yo strip (1.56x).  Every
+// cycles of work; 1.27x), against 336 for the 48 x 48 tiling with a yo strip (1.56x).  (r4,
+// measured and dropped: a cover of one 16x16 tile and ten 4x4x4_4b, 224 cycles, 1.04x, whose
+// extra operands cost more VALU issue than the matrix cycles it saves, 2-5% slower:
+// profiles/r4m_record_cover_ab.txt.)  Every
 // entry is one fp64 FMA chain over the columns in staging order, like the reference's
 // dsyrk/dgemv (products of fp32 values are exact in fp64).
 // The record kernel's fp64 side rows of a staged chunk (see assemble_record_kernel): per
@@ -819,193 +822,13 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
 }
 
 
-// assemble_record_blocks_kernel: the record of assemble_record_kernel with a tighter cover of
-// the 860 entries.  One 16x16x4 tile and ten v_mfma_f64_4x4x4_4b (4 blocks of 4x4 each):
-//   T1                 {16..31} x {0..15}                      (as above)
-//   P0, P1             tile t's off-diagonal 4x4 blocks (I, I-1 mod 4): A = the lane's own
-//                      row 16 t + m, B = row 16 t + (m - 4 mod 16), a row_ror:4 of it
-//   P2                 blocks (0,2), (1,3) of tile 0 and (2,0), (3,1) of tile 1: A = row m or
-//                      16 + m, B = row 8 + m, a row_ror:8
-//   D0, D1             tile t's diagonal blocks with one A row replaced by yo: row 4I+3 (t = 0)
-//                      or 16+4I (t = 1) gives b1 there and the block's other lower entries
-//                      come from its three rows (the upper ones mirror them)
-//   four strips        rows 32..39 x {0..31}                   (as above)
-//   one corner         32..35 with row 33 -> yo, x 32..35; 36..39 x 32..35; 36..39 with row
-//                      38 -> yo, x 36..39 (the fourth block is idle)
-// = 64 + 10 x 16 = 224 matrix-pipe cycles per 4 columns (1.04x the 215 of work, against 272
-// and 1.27x).  The ten diagonal entries the yo rows displaced, A(4I+3,4I+3), A(16+4I,16+4I),
-// A(33,33) and A(38,38), are one fp64 FMA per group on the lane that holds that row (summed
-// over the four column slots at the end).  The rotated B operands come from the lane's own
-// registers by DPP, so a group reads the same four fp32 rows and four fp64 side rows as above.
-struct RecordSideB {
-  static constexpr bool kPad = false;  // rows past 31 (but yo) are read from the side rows
-  RecordStripRows &s;
-  __device__ __forceinline__ void stage(int half, int sl, const f32x4 (&g)[kTq4KP / 8], float w) {
-    if (half) {  // rows 32..39 (this lane stages rows 20..39)
-      double *d = s.d[sl];
-      d[0] = (double)(g[3].x * w); d[1] = (double)(g[3].y * w);
-      d[2] = (double)(g[3].z * w); d[3] = (double)(g[3].w * w);
-      d[4] = (double)(g[4].x * w); d[5] = (double)(g[4].y * w);
-      d[6] = (double)(g[4].z * w); d[7] = (double)(g[4].w * w);
-    }
-  }
-  __device__ __forceinline__ void yo(int sl, float y) { s.d[sl][8] = (double)y; }
-};
-
-template <int WAVES>
-__global__ void __launch_bounds__(64, WAVES)
-assemble_record_blocks_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
-                              long long g0, int npts, const int *__restrict__ nbr_cnt,
-                              const int *__restrict__ nbr_idx, int2 *__restrict__ info,
-                              double *__restrict__ ws) {
-  constexpr int KP = kTq4KP, PITCH = 48, YO = KP;
-  static_assert(KP == 40 && MfmaLayout<KP>::PITCH == PITCH, "the cover is laid out for KP = 40");
-  using HO = AsmRecord<KP>;
-  __shared__ ColumnChunk<KP, kTqChunk, float, PITCH, true> ch;  // shifted columns (SWZ)
-  __shared__ RecordStripRows sr;
-  const int gi = xcd_remap(blockIdx.x, gridDim.x);
-  if (gi >= npts) return;
-  const int lane = threadIdx.x, kk = lane >> 4, m = lane & 15, x = m & 3;
-  float3 pt;
-  slab_point(slab, g0 + gi, pt.x, pt.y, pt.z);
-  // A rows of the diagonal blocks (yo in place of row 4 b + 3 / 16 + 4 b)
-  const int rD0 = x == 3 ? YO : m, rD1 = x == 0 ? YO : 16 + m;
-  // corner operands in the side rows (32..39 -> 0..7, yo -> 8), block b = m >> 2
-  const int bq = m >> 2;
-  const int cA = bq == 0 ? (x == 1 ? 8 : x) : bq == 1 ? 4 + x : bq == 2 ? (x == 2 ? 8 : 4 + x) : 0;
-  const int cB = bq == 0 ? x : bq == 1 ? x : bq == 2 ? 4 + x : 0;
-  const bool lo8 = m < 8;
-  // fixup lane: the diagonal entry this lane's column slot contributes to (-1: none)
-  const int fsel = x == 3 ? 0 : x == 0 ? 1 : m == 1 ? 2 : m == 2 ? 3 : 4;
-  f64x4 t1 = {0.0, 0.0, 0.0, 0.0};
-  double p0 = 0.0, p1 = 0.0, p2 = 0.0, d0 = 0.0, d1 = 0.0, cn = 0.0, fx = 0.0;
-  double st[4] = {0.0, 0.0, 0.0, 0.0};
-  // rows of the rotated and selected operands, read from the chunk like the others
-  const int rR0 = (m + 12) & 15, rR1 = 16 + ((m + 12) & 15), rQ8 = 8 + m, rPA = lo8 ? m : 16 + m;
-  const int rF = fsel == 0 ? m : fsel == 1 ? 16 + m : fsel == 2 ? 33 : fsel == 3 ? 38 : m;
-  const int ptot = stage_columns_pair<KP, kTqChunk, PITCH>(
-      ch, trees, c, gi, lane, nbr_cnt, nbr_idx, pt, [&](int nsl) {
-        float f[2][4];
-        double e[2][4];
-        const float *c0 = ch.col(kk);  // column 4 g + kk at c0 + g GSTRIDE
-        const double *dd0 = sr.d[kk];  // its side rows at dd0 + 48 g
-        auto load = [&](int b, int g) {
-          const float *col = c0 + g * ch.GSTRIDE;
-          f[b][0] = col[m];
-          f[b][1] = col[16 + m];
-          f[b][2] = col[rD0];
-          f[b][3] = col[rD1];
-          const double *dc = dd0 + 48 * g;
-          e[b][0] = dc[x];
-          e[b][1] = dc[4 + x];
-          e[b][2] = dc[cA];
-          e[b][3] = dc[cB];
-        };
-        const int nl = nsl;
-        if (nl > 0) load(0, 0);
-#pragma unroll
-        for (int g = 0; g < kTqChunk / 4; ++g) {
-          if (4 * g >= nl) break;  // nsl is wave-uniform
-          const int b = g & 1;
-          const float *col = c0 + g * ch.GSTRIDE;  // this group's other five operands
-          const float h0 = col[rR0], h1 = col[rR1], h2 = col[rQ8], h3 = col[rPA], h4 = col[rF];
-          const double o0 = (double)f[b][0], o1 = (double)f[b][1];
-          const double a0 = (double)f[b][2], a1 = (double)f[b][3];
-          const double s0 = e[b][0], s1 = e[b][1];
-          const double ca = e[b][2], cbv = e[b][3];
-          if (g + 1 < kTqChunk / 4 && 4 * (g + 1) < nl) load(b ^ 1, g + 1);
-          t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(o1, o0, t1, 0, 0, 0);
-          d0 = __builtin_amdgcn_mfma_f64_4x4x4f64(a0, o0, d0, 0, 0, 0);
-          d1 = __builtin_amdgcn_mfma_f64_4x4x4f64(a1, o1, d1, 0, 0, 0);
-          st[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(s0, o0, st[0], 0, 0, 0);
-          st[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(s1, o0, st[1], 0, 0, 0);
-          st[2] = __builtin_amdgcn_mfma_f64_4x4x4f64(s0, o1, st[2], 0, 0, 0);
-          st[3] = __builtin_amdgcn_mfma_f64_4x4x4f64(s1, o1, st[3], 0, 0, 0);
-          cn = __builtin_amdgcn_mfma_f64_4x4x4f64(ca, cbv, cn, 0, 0, 0);
-          const double r0 = (double)h0, r1 = (double)h1, q8 = (double)h2, pa = (double)h3;
-          const double fv = (double)h4;
-          p0 = __builtin_amdgcn_mfma_f64_4x4x4f64(o0, r0, p0, 0, 0, 0);
-          p1 = __builtin_amdgcn_mfma_f64_4x4x4f64(o1, r1, p1, 0, 0, 0);
-          p2 = __builtin_amdgcn_mfma_f64_4x4x4f64(pa, q8, p2, 0, 0, 0);
-          fx = fma(fv, fv, fx);
-        }
-      },
-      RecordSideB{sr});
-  if (lane == 0) info[gi] = make_int2(ptot, 0);  // p = 0: the solve leaves var unchanged
-  if (ptot == 0) return;
-  const int k = c.k;
-  const double inflat = (double)c.inflat;
-  double *__restrict__ w = ws + (long long)gi * HO::WORDS;
-  auto put = [&](int row, int col, double a) {  // packed lower; inflat on the live diagonal
-    w[HO::TA + row * (row + 1) / 2 + col] = row != col ? a : row < k ? a + inflat : 1.0;
-  };
-  auto b1 = [&](int row, double a) { w[HO::U1 + row] = a; };
-  // T1: A(16 + kk + 4 r, m)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) put(16 + kk + 4 * r, m, t1[r]);
-  // 4x4x4_4b results: lane (kk, 4 bq + x) = (row kk, column x) of block bq
-  {
-    // P0 / P1: block (bq, bq - 1 mod 4) of tile t; bq = 0 is (0, 3), stored mirrored
-    const int cj = 4 * ((bq + 3) & 3) + x, ri = 4 * bq + kk;
-    if (bq == 0) {
-      put(cj, ri, p0);
-      put(16 + cj, 16 + ri, p1);
-    } else {
-      put(ri, cj, p0);
-      put(16 + ri, 16 + cj, p1);
-    }
-    // P2: (0,2), (1,3) of tile 0 (mirrored), (2,0), (3,1) of tile 1
-    if (bq < 2) put(8 + 4 * bq + x, 4 * bq + kk, p2);
-    else put(16 + 4 * bq + kk, 16 + 4 * (bq - 2) + x, p2);
-    // D0: rows 4 bq + kk (kk = 3: yo), columns 4 bq + x
-    if (kk == 3) b1(4 * bq + x, d0);
-    else if (x <= kk) put(4 * bq + kk, 4 * bq + x, d0);
-    else if (x == 3) put(4 * bq + 3, 4 * bq + kk, d0);
-    // D1: rows 16 + 4 bq + kk (kk = 0: yo), columns 16 + 4 bq + x
-    if (kk == 0) b1(16 + 4 * bq + x, d1);
-    else if (x <= kk) put(16 + 4 * bq + kk, 16 + 4 * bq + x, d1);
-    // strips: A(32 + 4 r + kk, 16 J + m)
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int J = 0; J < 2; ++J) put(32 + 4 * r + kk, 16 * J + m, st[2 * J + r]);
-    // corner
-    if (bq == 0) {  // rows 32..35 (33: yo) x 32..35
-      if (kk == 1) b1(32 + x, cn);
-      else if (x <= kk) put(32 + kk, 32 + x, cn);
-      else if (x == 1) put(33, 32 + kk, cn);
-    } else if (bq == 1) {  // 36..39 x 32..35
-      put(36 + kk, 32 + x, cn);
-    } else if (bq == 2) {  // rows 36..39 (38: yo) x 36..39
-      if (kk == 2) b1(36 + x, cn);
-      else if (x <= kk) put(36 + kk, 36 + x, cn);
-      else if (x == 2) put(38, 36 + kk, cn);
-    }
-  }
-  // the displaced diagonal entries: sum of the four column slots' partials
-  const double fsum = (fx + __shfl_xor(fx, 16, 64)) + (__shfl_xor(fx, 32, 64) +
-                                                      __shfl_xor(__shfl_xor(fx, 16, 64), 32, 64));
-  if (kk == 0 && fsel < 4) {
-    const int row = fsel == 0 ? m : fsel == 1 ? 16 + m : fsel == 2 ? 33 : 38;
-    put(row, row, fsum);
-  }
-}
-
 hipError_t launch_assemble_record(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
                                   SlabDev slab, long long g0, int npts, const int *nbr_cnt,
                                   const int *nbr_idx, int2 *info, double *ws) {
   if (npts <= 0) return hipSuccess;
   if (kp != kTq4KP) return hipErrorInvalidValue;
-  static const bool blocks = [] {
-    const char *e = getenv("CWBL_ASM_COVER");
-    return !(e && atoi(e) == 0);
-  }();
-  if (blocks)
-    hipLaunchKernelGGL((assemble_record_blocks_kernel<kRecordWaves>), dim3(npts), dim3(64), 0, s,
-                       trees, c, slab, g0, npts, nbr_cnt, nbr_idx, info, ws);
-  else
-    hipLaunchKernelGGL((assemble_record_kernel<kRecordWaves>), dim3(npts), dim3(64), 0, s, trees,
-                       c, slab, g0, npts, nbr_cnt, nbr_idx, info, ws);
+  hipLaunchKernelGGL((assemble_record_kernel<kRecordWaves>), dim3(npts), dim3(64), 0, s, trees,
+                     c, slab, g0, npts, nbr_cnt, nbr_idx, info, ws);
   return hipGetLastError();
 }
 
