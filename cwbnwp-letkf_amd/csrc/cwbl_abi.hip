@@ -239,7 +239,6 @@ struct State {
   int tq4 = 1;  // CWBL_TQ4: KP=40 solve 0 = one kernel, else assembly record + solve_tq40
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: record batch (points)
   bool big_split = true;                              // CWBL_BIG_SPLIT=0: one-kernel KP=128 solve
-  bool big_streams = false;  // CWBL_BIG_STREAMS=1: the split k > 64 path's tail on its own stream
   long long big_sub = 98304;                          // CWBL_BIG_SUB: KP=128 hand-off batch
   std::vector<hipEvent_t> events;
   hipStream_t h2d = nullptr, d2h = nullptr;           // host-memory slab copies (pipelined)
@@ -743,8 +742,6 @@ int cwbl_init(const cwbl_init_params *p) {
   if (const char *e = std::getenv("CWBL_PAGEABLE")) S.pageable_register = std::strcmp(e, "bounce") != 0;
   S.bin_div = 0;  // 0: by density (bin_div_for)
   if (const char *e = std::getenv("CWBL_BIN_DIV")) S.bin_div = std::max(1, std::min(8, std::atoi(e)));
-  S.big_streams = false;
-  if (const char *e = std::getenv("CWBL_BIG_STREAMS")) S.big_streams = std::atoi(e) != 0;
   if (const char *e = std::getenv("CWBL_BIG_SUB")) S.big_sub = std::max(64LL, std::atoll(e));
   if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
   S.serial_search = false;
@@ -1104,10 +1101,9 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   // reduction two search batches back (info reuse).
   const bool big_split_path = (S.kp == 96 || S.kp == kBigSplitKP) && S.big_split &&
                               S.k > big_split_j0(S.kp) + 2;
-  // (the same two-stream scheme for the k > 64 split path: the one-wavefront tail of a
-  // hand-off sub-batch beside the next sub-batch's 256-thread kernel, CWBL_BIG_STREAMS)
-  const bool conc = (S.tq40_streams && S.tq4 && S.kp == kTq4KP && !S.jacobi) ||
-                    (S.big_streams && big_split_path);
+  // (r4, measured and dropped: the same two-stream scheme for the k > 64 split path, the
+  // tail of a hand-off sub-batch beside the next sub-batch's 256-thread kernel: +0.5%)
+  const bool conc = S.tq40_streams && S.tq4 && S.kp == kTq4KP && !S.jacobi;
   int nrec = 0;                 // record batches so far
   std::vector<int> rec_done;    // cevent after each record batch's solve (on S.tstream)
   std::vector<int> info_done;   // cevent after each search batch's info reduction
@@ -1180,33 +1176,6 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       long long Bs = (nb + nsub - 1) / nsub;
       Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
       HIPCHK(S.wsa.ensure((size_t)Bs * rec_bytes));
-      if (conc) {  // two hand-off and two info buffers (see the record path below)
-        HIPCHK(S.wsa2.ensure((size_t)Bs * rec_bytes));
-        int2 *binfo = (bi & 1) ? S.info2.as<int2>() : S.info.as<int2>();
-        if (bi >= 2) HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[info_done[bi - 2]], 0));
-        for (long long s0 = 0; s0 < nb; s0 += Bs) {
-          const int ns = (int)std::min<long long>(Bs, nb - s0);
-          double *recp = (nrec & 1) ? S.wsa2.as<double>() : S.wsa.as<double>();
-          if (nrec >= 2)  // this hand-off buffer: finished by the tail two sub-batches back
-            HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[rec_done[nrec - 2]], 0));
-          HIPCHK(kt_begin(S.stream, &kt));
-          HIPCHK(launch_big_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,
-                                    nidx + s0 * list_cap, binfo + s0, recp));
-          HIPCHK(kt_end(S.stream, kt, KT_BIG_HANDOFF, ns));
-          hipEvent_t ea, et;
-          HIPCHK(cevent(cev, &ea));
-          HIPCHK(cevent(cev + 1, &et));
-          HIPCHK(hipEventRecord(ea, S.stream));
-          HIPCHK(hipStreamWaitEvent(S.tstream, ea, 0));
-          HIPCHK(kt_begin(S.tstream, &kt));
-          HIPCHK(launch_solve_tqb_tail(S.tstream, S.kp, c, sd, g0 + s0, ns, recp, binfo + s0));
-          HIPCHK(kt_end(S.tstream, kt, KT_TQB_TAIL, ns));
-          HIPCHK(hipEventRecord(et, S.tstream));
-          rec_done.push_back(cev + 1);
-          cev += 2;
-          ++nrec;
-        }
-      } else
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
         const int ns = (int)std::min<long long>(Bs, nb - s0);
         HIPCHK(kt_begin(S.stream, &kt));
