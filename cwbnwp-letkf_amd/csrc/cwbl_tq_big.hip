@@ -345,6 +345,23 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     const double2 a1 = *reinterpret_cast<const double2 *>(p + 2);
     o[0] = a0.x; o[1] = a0.y; o[2] = a1.x; o[3] = a1.y;
   };
+  // The step's 4-value groups in LDS (v, w: group x = rows 4x..4x+3; the A v partials: block
+  // row R) keep their two halves swapped when bit 3 of the group index is set (hsw), so that
+  // the 16 lanes of a 16-B access, whose groups are mostly 16 consecutive ones (32 B apart),
+  // hit all 64 banks once instead of half of them twice (r4: LDS bank conflicts were 82% of
+  // the kernel's LDS-active cycles, profiles/r4n_c4_sq_counters.txt).  Element i of v or w
+  // lives at i ^ (hsw(i >> 2) << 1).
+  auto hsw = [](int x) { return (x >> 3) & 1; };
+  auto ld4s = [](const double *p, int sw, double (&o)[4]) {  // logical half 0 at p + 2 sw
+    const double2 a0 = *reinterpret_cast<const double2 *>(p + 2 * sw);
+    const double2 a1 = *reinterpret_cast<const double2 *>(p + 2 - 2 * sw);
+    o[0] = a0.x; o[1] = a0.y; o[2] = a1.x; o[3] = a1.y;
+  };
+  auto st4s = [](double *p, int sw, double a0, double a1, double a2, double a3) {
+    *reinterpret_cast<double2 *>(p + 2 * sw) = make_double2(a0, a1);
+    *reinterpret_cast<double2 *>(p + 2 - 2 * sw) = make_double2(a2, a3);
+  };
+  const int tsw = tid ^ (hsw(tid >> 2) << 1);  // this thread's element of v and w
   // column j of the lower block triangle -> dst (4 rows per block of block column j/4); the
   // column within the block is uniform, so a switch picks it (no per-value selects)
   auto pub4 = [](double *d, double a0, double a1, double a2, double a3) {
@@ -408,7 +425,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     // are skipped below, and the row sums rely on every block's last live step
     // (j = 4 bj + 3, where v vanishes on its columns) leaving exact zeros in its A v partials.
     const double v = tid == j + 1 ? 1.0 : x * scal;
-    if (tid < KP) sm.vb[tid] = v;
+    if (tid < KP) sm.vb[tsw] = v;
     if (tid == j + 1) {  // x'_{j+1}, b1_{j+1} for every thread's v.x', v.b1
       sm.piv[0] = ux;
       sm.piv[1] = ub;
@@ -419,8 +436,8 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     for (int it = 0; it < NBL; ++it) {
       if (tid + NT * it < NBLK && bj[it] >= J) {
         double vi[4], vj[4];
-        ld4(&sm.vb[4 * bi[it]], vi);
-        ld4(&sm.vb[4 * bj[it]], vj);
+        ld4s(&sm.vb[4 * bi[it]], hsw(bi[it]), vi);
+        ld4s(&sm.vb[4 * bj[it]], hsw(bj[it]), vj);
         double pr[4], pc[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -437,15 +454,10 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
         double sp = vi[0] * pr[0];
 #pragma unroll
         for (int r = 1; r < 4; ++r) sp = fma(vi[r], pr[r], sp);
-        double *dst = &sm.u.pb[bi[it]][4 * bj[it]];
-        *reinterpret_cast<double2 *>(dst) = make_double2(pr[0], pr[1]);
-        *reinterpret_cast<double2 *>(dst + 2) = make_double2(pr[2], pr[3]);
+        st4s(&sm.u.pb[bi[it]][4 * bj[it]], hsw(bi[it]), pr[0], pr[1], pr[2], pr[3]);
         if (bi[it] != bj[it]) {
-          if (bj[it] >= J) {
-            double *dt = &sm.u.pb[bj[it]][4 * bi[it]];
-            *reinterpret_cast<double2 *>(dt) = make_double2(pc[0], pc[1]);
-            *reinterpret_cast<double2 *>(dt + 2) = make_double2(pc[2], pc[3]);
-          }
+          if (bj[it] >= J)
+            st4s(&sm.u.pb[bj[it]][4 * bi[it]], hsw(bj[it]), pc[0], pc[1], pc[2], pc[3]);
           sp = sp + sp;
         }
         s1p += sp;
@@ -458,7 +470,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     s1 *= tau;               // p . v with p = tau A v
     double pp = 0.0;
     if (tid < KP && tid > j) {
-      const double *prow = &sm.u.pb[tid >> 2][tid & 3];
+      const double *prow = &sm.u.pb[tid >> 2][tsw & 3];
       // block columns < J hold exact zeros (dead blocks): start at the 8-column segment of J
       auto rsum = [&](auto C) {
         constexpr int c0 = decltype(C)::value;
@@ -475,16 +487,16 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     }
     const double p = (tid > j && tid < k) ? tau * pp : 0.0;
     const double w = fma(-0.5 * tau * s1, v, p);
-    if (tid < KP) sm.wb[tid] = w;
+    if (tid < KP) sm.wb[tsw] = w;
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < NBL; ++it) {
       if (tid + NT * it < NBLK && bj[it] >= J) {
         double vi[4], vj[4], wi[4], wj[4];
-        ld4(&sm.vb[4 * bi[it]], vi);
-        ld4(&sm.vb[4 * bj[it]], vj);
-        ld4(&sm.wb[4 * bi[it]], wi);
-        ld4(&sm.wb[4 * bj[it]], wj);
+        ld4s(&sm.vb[4 * bi[it]], hsw(bi[it]), vi);
+        ld4s(&sm.vb[4 * bj[it]], hsw(bj[it]), vj);
+        ld4s(&sm.wb[4 * bi[it]], hsw(bi[it]), wi);
+        ld4s(&sm.wb[4 * bj[it]], hsw(bj[it]), wj);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll

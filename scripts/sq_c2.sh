@@ -12,7 +12,7 @@ PB="SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT
 i=0
 for P in "$PA" "$PB"; do
   i=$((i+1))
-  timeout -s KILL 240 rocprofv3 --pmc $P --kernel-include-regex "assemble|tq40" -d $OUT/p$i -o p$i --output-format csv -- $B > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc $P --kernel-include-regex "${KREGEX:-assemble|tq40}" -d $OUT/p$i -o p$i --output-format csv -- $B > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 python3 - $OUT <<'PY' | tee $OUT/summary.txt
 import csv, glob, sys, collections
