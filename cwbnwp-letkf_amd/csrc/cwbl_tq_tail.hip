@@ -171,19 +171,31 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     // xt_{j+1} = alpha - beta = 1/scal (0 when H = I), so column j + 1 needs no special
     // case (v_{j+1} = scal (alpha - beta) is 1 to the last bit or so).
     const double amb = nz ? alpha - bt : 0.0;
-    // A v = scal * sum_{c >= j+1} A(:, c) xt_c; x_c from lane jl, a group's eight broadcasts
-    // first (16 SGPRs), then its FMAs; groups left of column j + 1 are skipped
+    // A v = scal * sum_{c >= j+1} A(:, c) xt_c; x_c = A(j, c) from the published row (LDS
+    // broadcasts; r4: instead of 16 v_readlane and 8 scalar selects per group), the selects
+    // only in the group of column j + 1; groups left of it are skipped
     double q[4] = {0.0, 0.0, 0.0, 0.0};  // four chains
     sfor<NG>([&](auto gg) {
       constexpr int c0 = 8 * decltype(gg)::value;
       if (c0 + 7 >= j1) {
         double xs[8];
-        sfor<8>([&](auto ii) { xs[ii] = readlane_f64(A[c0 + ii], jl); });
-        sfor<8>([&](auto ii) {
-          constexpr int col = c0 + decltype(ii)::value;
-          const double xt = col > j1 ? xs[ii] : col == j1 ? amb : 0.0;  // scalar selects
-          q[col % 4] = fma(A[col], xt, q[col % 4]);
+        sfor<4>([&](auto ii) {
+          const double2 x2 = *reinterpret_cast<const double2 *>(&sm.row[c0 + 2 * ii]);
+          xs[2 * ii] = x2.x;
+          xs[2 * ii + 1] = x2.y;
         });
+        if (c0 > j1) {
+          sfor<8>([&](auto ii) {
+            constexpr int col = c0 + decltype(ii)::value;
+            q[col % 4] = fma(A[col], xs[ii], q[col % 4]);
+          });
+        } else {  // the group of column j + 1
+          sfor<8>([&](auto ii) {
+            constexpr int col = c0 + decltype(ii)::value;
+            const double xt = col > j1 ? xs[ii] : col == j1 ? amb : 0.0;
+            q[col % 4] = fma(A[col], xt, q[col % 4]);
+          });
+        }
       }
     });
     const double av = scal * ((q[0] + q[1]) + (q[2] + q[3]));  // (A v)_l
