@@ -114,3 +114,27 @@ def test_c3_eight_ranks_full_c2_grid(tmp_path):
     1e-6."""
     _sharded_run_equals_single_process_and_oracle(
         tmp_path, 8, dict(name="c2"), workspace=512 << 20, block=(144, 144, 12))
+
+
+@pytest.mark.timeout(900)
+def test_bench_two_ranks_end_to_end():
+    """`bench.py --gpus 2` end to end, as the driver's scaling run starts it (the script launches
+    its own ranks under torch.distributed.run), with both ranks on this GPU over gloo: the
+    obs-set broadcast, the sharded analysis, the member<->column transposes and the 16-variable
+    cycle with write_mean, ending in one JSON line whose n_gpus counts distinct devices."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CWBL_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--no-cpu-baseline", "--no-detail-configs"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=850)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 1 and d["config"]["ranks"] == 2 and d["value"] > 0
+    t = d["detail"]["transposes"]
+    assert t["scatter_ms"] > 0 and t["gather_ms"] > 0
+    cy = d["detail"]["cycle"]
+    assert cy["transposes"] is True and cy["variables"] == 16 and cy["write_mean_ms"] > 0
