@@ -526,7 +526,8 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
                               hipMemcpyHostToDevice, S.stream));
       build_bins(h, tdim, std::sqrt(search_r2()), nt->bins, bin_div_for(h, tdim));
       const HostBins &hb = nt->bins;
-      HIPCHK(nt->bxyz.ensure(hb.xyzs.size() * sizeof(float) + 16));
+      // (+ kBinPad points: search_binned_kernel reads up to 7 points past a run's end)
+      HIPCHK(nt->bxyz.ensure(hb.xyzs.size() * sizeof(float) + 16 * kBinPad));
       HIPCHK(nt->bstart.ensure(hb.start.size() * sizeof(int)));
       if (!hb.xyzs.empty())
         HIPCHK(hipMemcpyAsync(nt->bxyz.p, hb.xyzs.data(), hb.xyzs.size() * sizeof(float),
@@ -976,6 +977,10 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   if (!S.max_batch_set) B = std::min<long long>(B, std::max<long long>(npts / 6, 64000));
   B = std::max<long long>(std::min<long long>(B, npts), 256);
   B = std::min<long long>(B, 1 << 22);
+  // a batch's lists stay below 4 GiB: search_binned_kernel addresses them by 32-bit offsets
+  if (list_cap > 0)
+    B = std::min<long long>(B, (long long)((((size_t)1 << 32) - 1) / ((size_t)list_cap * 4)) /
+                                   kListLanes * kListLanes);
   // Batch plan: the first batch's search cannot overlap a solve, so it is short (a lead of
   // 1/lead_div of the points); the rest are equal (a short last batch is all tail) and
   // whole list groups.

@@ -213,6 +213,12 @@ __device__ __forceinline__ T gld(const T *base, unsigned i) {
   const char *b = reinterpret_cast<const char *>(base) + (unsigned)(i * (unsigned)sizeof(T));
   return *gptr(reinterpret_cast<const T *>(b));
 }
+// *(T *)((char *)base + byteoff) = v, a global store at SGPR base + 32-bit offset
+template <class T>
+__device__ __forceinline__ void gst(T *base, unsigned byteoff, T v) {
+  char *b = reinterpret_cast<char *>(base) + byteoff;
+  *(__attribute__((address_space(1))) T *)reinterpret_cast<T *>(b) = v;
+}
 __device__ __forceinline__ f32x4 gld4(const float *base, unsigned i) {  // 16 B at base + 4i
   const char *b = reinterpret_cast<const char *>(base) + (unsigned)(i * 4u);
   return *gptr(reinterpret_cast<const f32x4 *>(b));

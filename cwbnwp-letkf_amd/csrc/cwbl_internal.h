@@ -279,6 +279,8 @@ constexpr int kSearchStackDepth = 40;  // max k-d tree depth the search kernel s
 // round_up(npts, kListLanes) * cap entries.
 constexpr int kListLanes = 64;
 constexpr int kListGroup = 4;
+// points of padding after a tree's bins: search_binned_kernel reads ahead past a run's end
+constexpr int kBinPad = 8;
 __host__ __device__ inline int list_span(int max_lz) {
   return (max_lz + kListGroup - 1) / kListGroup * kListGroup;
 }

@@ -313,7 +313,9 @@ hipError_t launch_search(hipStream_t s, const TreeDesc *trees, int ntrees, int d
 // the fp64 sums of the solve.  Where kdtree2's order decides WHICH points are kept (a list
 // past max_lz, Q4) the point is flagged and search_kernel<FlagQuery> redoes it.
 // ---------------------------------------------------------------------------------------
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBinAhead = 8;  // bin points loaded ahead of their tests
+static_assert(kBinAhead <= kBinPad, "the look-ahead stays inside the bins' padding");
 __global__ void __launch_bounds__(64)
 search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_cap, float r2,
                      float rbox, SlabQuery qs, int npts, int *__restrict__ nbr_cnt,
@@ -322,6 +324,7 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
   // (r4, measured and dropped: an XCD-aware block order, a tie at C2 and C5; four lanes per
   // point, which cuts this kernel's time by 25% at C2 and 38% at C5 but, overlapped with the
   // assembly, costs the step 1-2% at C2 through its extra issue cycles: profiles/r4k_*)
+  __shared__ __attribute__((aligned(16))) int sgrp[64][4];
   const int gi = blockIdx.x * 64 + threadIdx.x;
   if (gi >= npts) return;
   float px, py, pz;
@@ -331,11 +334,12 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
     const TreeDesc &T = trees[t];
     const float q0 = px * T.hclr_inv, q1 = py * T.hclr_inv;  // get_lz (:243-253)
     const float q2 = T.query3d ? pz * T.vclr_inv : 0.0f;
-    int *__restrict__ out = nbr_idx + list_index(gi, list_cap, T.list_off);
+    // this point's list: byte offset from nbr_idx (the list buffer stays below 2 GiB)
+    const unsigned obase = 4u * (unsigned)list_index(gi, list_cap, T.list_off);
+    int *grp = sgrp[threadIdx.x];  // this lane's group of 4 list slots
     const int dim = T.tree_dim, max_lz = T.max_lz;
     int count = 0;
     bool ovf = false;
-    int4 grp = make_int4(0, 0, 0, 0);
     if (max_lz > 0) {
       // conservative cell range of [q - rbox, q + rbox] (clamped before the int conversion)
       // (the margin also covers the rounding of q -/+ rbox and of the cell arithmetic, which
@@ -360,9 +364,9 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
         const float g = fmaxf(fmaxf(lo - q, q - hi), 0.0f);
         return fmaxf(g - 1e-3f * h - margin(q, b0), 0.0f);
       };
-      for (int iz = iz0; iz <= iz1 && !ovf; ++iz) {
+      for (int iz = iz0; iz <= iz1; ++iz) {
         const float gz = dim == 3 ? gap(q2, T.bz0, iz) : 0.0f;
-        for (int iy = iy0; iy <= iy1 && !ovf; ++iy) {
+        for (int iy = iy0; iy <= iy1; ++iy) {
           // the ball's x-extent over this row of cells
           const float gy = gap(q1, T.by0, iy);
           const float rem = rb2 - gy * gy - gz * gz;
@@ -374,11 +378,14 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
                                                (float)(T.nbx - 1)));
           if (jx0 > jx1) continue;
           const int cb = (iz * T.nby + iy) * T.nbx;
-          const int e = T.bstart[cb + jx1 + 1];
-          for (int i0 = T.bstart[cb + jx0]; i0 < e; i0 += kBinAhead) {
-            float4 d[kBinAhead];
+          const int e = gld(T.bstart, (unsigned)(cb + jx1 + 1));
+          // global loads at SGPR base + 32-bit offset; the points past e that a round reads
+          // (at most kBinAhead - 1, never accepted) stay inside the array's padding
+          const float *bx = reinterpret_cast<const float *>(T.bxyz);
+          for (int i0 = gld(T.bstart, (unsigned)(cb + jx0)); i0 < e; i0 += kBinAhead) {
+            f32x4 d[kBinAhead];
 #pragma unroll
-            for (int a = 0; a < kBinAhead; ++a) d[a] = T.bxyz[min(i0 + a, e - 1)];
+            for (int a = 0; a < kBinAhead; ++a) d[a] = gld4(bx, 4u * (unsigned)(i0 + a));
 #pragma unroll
             for (int a = 0; a < kBinAhead; ++a) {
               const float dx = d[a].x - q0, dy = d[a].y - q1;
@@ -388,28 +395,30 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
                 const float dz = d[a].z - q2;
                 sd = sd + dz * dz;
               }
-              if (i0 + a < e && sd <= r2 && !ovf) {
-                if (count == max_lz) {
-                  ovf = true;
-                } else {
-                  const int slot = __float_as_int(d[a].w);
-                  const int g = count % kListGroup;
-                  grp.x = g == 0 ? slot : grp.x;
-                  grp.y = g == 1 ? slot : grp.y;
-                  grp.z = g == 2 ? slot : grp.z;
-                  grp.w = slot;
-                  if (g == kListGroup - 1)
-                    *reinterpret_cast<int4 *>(out + list_slot(count - g)) = grp;
-                  ++count;
+              // a hit goes to this lane's 4-slot group in LDS, a full group to the list as
+              // one 16-B store; hits past max_lz are counted, not stored: count > max_lz is
+              // the overflow (Q4)
+              if (i0 + a < e && sd <= r2) {
+                if (count < max_lz) {
+                  grp[count & 3] = __float_as_int(d[a].w);
+                  if ((count & 3) == 3)
+                    gst(reinterpret_cast<i32x4 *>(nbr_idx), obase + 4u * list_slot(count - 3),
+                        *reinterpret_cast<const i32x4 *>(grp));
                 }
+                ++count;
               }
             }
-            if (ovf) break;
+            if (count > max_lz) break;
           }
+          if (count > max_lz) break;
         }
+        if (count > max_lz) break;
       }
-      if (count % kListGroup != 0)
-        *reinterpret_cast<int4 *>(out + list_slot(count - count % kListGroup)) = grp;
+      ovf = count > max_lz;
+      count = min(count, max_lz);
+      if (count & 3)  // the last, partial group (its slots past count are never read)
+        gst(reinterpret_cast<i32x4 *>(nbr_idx), obase + 4u * list_slot(count & ~3),
+            *reinterpret_cast<const i32x4 *>(grp));
     }
     nbr_cnt[(long long)gi * ntrees + t] = count;
     flagged = flagged || ovf;
