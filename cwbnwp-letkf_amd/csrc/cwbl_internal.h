@@ -288,8 +288,8 @@ __host__ __device__ inline long long list_index(long long g, int cap, int off) {
   return (g / kListLanes) * (long long)cap * kListLanes + (long long)off * kListLanes +
          (g % kListLanes) * kListGroup;
 }
-__host__ __device__ inline unsigned list_slot(int s) {
-  return (unsigned)(s / kListGroup) * (kListGroup * kListLanes) + (unsigned)(s % kListGroup);
+__host__ __device__ inline unsigned list_slot(int s) {  // s >= 0
+  return (unsigned)s / kListGroup * (kListGroup * kListLanes) + (unsigned)s % kListGroup;
 }
 
 int supported_kp(int k);      // smallest compiled KP >= k, or -1

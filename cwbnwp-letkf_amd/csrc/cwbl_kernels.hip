@@ -401,8 +401,8 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
               if (i0 + a < e && sd <= r2) {
                 if (count < max_lz) {
                   grp[count & 3] = __float_as_int(d[a].w);
-                  if ((count & 3) == 3)
-                    gst(reinterpret_cast<i32x4 *>(nbr_idx), obase + 4u * list_slot(count - 3),
+                  if ((count & 3) == 3)  // slot count - 3 = count & ~3 starts the group
+                    gst(reinterpret_cast<i32x4 *>(nbr_idx), obase + 4u * list_slot(count & ~3),
                         *reinterpret_cast<const i32x4 *>(grp));
                 }
                 ++count;
