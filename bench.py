@@ -633,7 +633,7 @@ def main():
 
     for _ in range(args.warmup):
         core.analyze_var(w.vp, slab)
-    core.set_kernel_timing(True)
+    core.set_kernel_timing(os.environ.get("CWBL_BENCH_KT", "1") != "0")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
