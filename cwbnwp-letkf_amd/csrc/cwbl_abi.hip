@@ -1095,7 +1095,6 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     HIPCHK(S.nbr_cnt2.ensure(bytes_cnt));
     HIPCHK(S.nbr_idx2.ensure(bytes_idx));
   }
-  HIPCHK(S.info.ensure((size_t)B * sizeof(int2)));
   HIPCHK(S.flags.ensure((size_t)(B + 1) * sizeof(int)));
   // bounding-box half-width of the binned search: the radius with a margin, so that every
   // point with d2 <= r2 in fp32 lies inside
@@ -1132,10 +1131,15 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   int nrec = 0;                 // record batches so far
   std::vector<int> rec_done;    // cevent after each record batch's solve (on S.tstream)
   std::vector<int> info_done;   // cevent after each search batch's info reduction
+  // one-stream path: the info of the whole call, reduced once after the last batch (a
+  // reduction kernel per batch cost the C2 step ~0.5 ms); the two-stream record path
+  // alternates two batch-sized buffers, reduced per batch
+  HIPCHK(S.info.ensure((size_t)(conc ? B : std::max<long long>(B, npts)) * sizeof(int2)));
   if (conc) HIPCHK(S.info2.ensure((size_t)B * sizeof(int2)));
   for (long long bi = 0; bi < nbat; ++bi) {
     const long long g0 = plan[bi].first;
     const int nb = plan[bi].second;
+    int2 *const infob = S.info.as<int2>() + (conc ? 0 : g0);  // this batch's info (one stream)
     int *ncnt = (bi & 1) ? S.nbr_cnt2.as<int>() : S.nbr_cnt.as<int>();
     int *nidx = (bi & 1) ? S.nbr_idx2.as<int>() : S.nbr_idx.as<int>();
     hipEvent_t a, b, b2, cc, dn;
@@ -1205,24 +1209,24 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
         const int ns = (int)std::min<long long>(Bs, nb - s0);
         HIPCHK(kt_begin(S.stream, &kt));
         HIPCHK(launch_big_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,
-                                  nidx + s0 * list_cap, S.info.as<int2>() + s0,
+                                  nidx + s0 * list_cap, infob + s0,
                                   S.wsa.as<double>()));
         HIPCHK(kt_end(S.stream, kt, KT_BIG_HANDOFF, ns));
         HIPCHK(kt_begin(S.stream, &kt));
         HIPCHK(launch_solve_tqb_tail(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
-                                     S.info.as<int2>() + s0));
+                                     infob + s0));
         HIPCHK(kt_end(S.stream, kt, KT_TQB_TAIL, ns));
       }
     } else if (S.kp > kMaxWaveKP) {
       HIPCHK(kt_begin(S.stream, &kt));
       HIPCHK(launch_solve_tq_big(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
                                  nullptr, nullptr, nullptr, nullptr, nullptr,
-                                 S.info.as<int2>()));
+                                 infob));
       HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ_BIG, nb));
     } else if (S.jacobi) {
       HIPCHK(kt_begin(S.stream, &kt));
       HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, ncnt, nidx,
-                                    S.info.as<int2>()));
+                                    infob));
       HIPCHK(kt_end(S.stream, kt, KT_SOLVE_JACOBI, nb));
     } else if (S.tq4 && S.kp == kTq4KP) {
       // assembly -> workspace -> four-points-per-wave solve, in hand-off batches of Bs
@@ -1238,7 +1242,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       const size_t wbytes = (size_t)(Bs + 1) * 8 * AsmRecord<kTq4KP>::WORDS;
       HIPCHK(S.wsa.ensure(wbytes));
       if (conc) HIPCHK(S.wsa2.ensure(wbytes));
-      int2 *binfo = conc && (bi & 1) ? S.info2.as<int2>() : S.info.as<int2>();
+      int2 *binfo = conc && (bi & 1) ? S.info2.as<int2>() : infob;
       if (conc && bi >= 2)  // this search batch's info buffer: reduced two batches back
         HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[info_done[bi - 2]], 0));
       for (long long s0 = 0; s0 < nb; s0 += Bs) {
@@ -1267,22 +1271,22 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
         } else if (ns == nb) {  // the whole batch: timed between b2 and dn (recorded anyway)
           auto asm_ = [&]() {
             return launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0, ns, ncnt, nidx,
-                                          S.info.as<int2>(), S.wsa.as<double>());
+                                          infob, S.wsa.as<double>());
           };
           auto tq40 = [&]() {
             return launch_solve_tq40(S.stream, S.kp, c, sd, g0, ns, S.wsa.as<double>(),
-                                     S.info.as<int2>());
+                                     infob);
           };
           HIPCHK(kt_pair(S.stream, b2, KT_ASSEMBLE_RECORD, ns, dn, KT_SOLVE_TQ40, ns, asm_, tq40));
         } else {
           HIPCHK(kt_begin(S.stream, &kt));
           HIPCHK(launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
                                         ncnt + s0 * nt, nidx + s0 * list_cap,
-                                        S.info.as<int2>() + s0, S.wsa.as<double>()));
+                                        infob + s0, S.wsa.as<double>()));
           HIPCHK(kt_end(S.stream, kt, KT_ASSEMBLE_RECORD, ns));
           HIPCHK(kt_begin(S.stream, &kt));
           HIPCHK(launch_solve_tq40(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
-                                   S.info.as<int2>() + s0));
+                                   infob + s0));
           HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ40, ns));
         }
       }
@@ -1290,7 +1294,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       HIPCHK(kt_begin(S.stream, &kt));
       HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
                              nullptr, nullptr, nullptr, nullptr, nullptr,
-                             S.info.as<int2>()));
+                             infob));
       HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ, nb));
     }
     HIPCHK(hipEventRecord(dn, S.stream));  // this batch's lists are free again
@@ -1302,9 +1306,8 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       HIPCHK(cevent(cev, &ir));
       HIPCHK(hipEventRecord(ir, S.tstream));
       info_done.push_back(cev++);
-    } else {
-      HIPCHK(hipEventRecord(cc, S.stream));
-      HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), nb, dst));
+    } else {  // the solve's end is dn's point on S.stream: no second event there
+      cc = dn;
     }
     if (piped_back) {  // the batch's analysis back to the caller behind its last solve
       HIPCHK(hipStreamWaitEvent(S.d2h, cc, 0));
@@ -1330,12 +1333,13 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
         if (int rc = bounce_drain(bi - (State::kSlots - 1))) return rc;
     }
     search_ev.push_back({ev, ev + 1});
-    solve_ev.push_back({ev + 2, ev + 3});
+    solve_ev.push_back({ev + 2, conc ? ev + 3 : ev + 4});
     done_ev.push_back(ev + 4);
     ev += 5;
   }
   if (conc && !info_done.empty())  // everything below follows the last solve and reduction
     HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[info_done.back()], 0));
+  if (!conc && npts > 0) HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), (int)npts, dst));
   if (vp->tune_q) {  // letkf_driver's Q species post-step (:253-278), on the resident slab
     hipEvent_t a, b;
     HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b));
