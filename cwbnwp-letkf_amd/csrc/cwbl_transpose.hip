@@ -40,39 +40,34 @@ void make_decomp(Decomp &d, int nx, int ny, int nz, int px, int py) {
   for (int b = 0; b < py; ++b) { d.rows_before[b] = acc; acc += cyc_count(ny, b, py); }
 }
 
-// element (x, y, z) of global(nx,ny,nz) -> its position in the rank-major chunk buffer
-__device__ inline long long chunk_pos(const Decomp &d, int x, int y, int z) {
-  const int idx = x % d.px, i = x / d.px;
-  const int idy = y % d.py, j = y / d.py;
-  const long long lnx = cyc_count(d.nx, idx, d.px), lny = cyc_count(d.ny, idy, d.py);
-  // ranks r' < r = idx + idy*px: whole rows of the rank grid, then this row's left part
+// Element (x, y, z) of global(nx,ny,nz) goes to its position in the rank-major chunk buffer
+// (line_pos).  One block row per (y, z) line of the field (blockIdx.y = y, blockIdx.z = z), threads along
+// x: the row's rank-grid row and offsets are block-uniform, and a thread does one 32-bit
+// division (x by px) instead of the 64-bit element decomposition (r4: the kernels were
+// integer-division bound at ~0.7 TB/s).
+constexpr int kPackThreads = 128;
+__device__ inline long long line_pos(const Decomp &d, int x, int y, int z) {
+  const int idy = y % d.py, j = y / d.py;   // block-uniform
+  const int lny = cyc_count(d.ny, idy, d.py);
+  const int i = x / d.px, idx = x - i * d.px;
+  const int lnx = cyc_count(d.nx, idx, d.px);
   const long long base = (long long)d.nz * ((long long)d.rows_before[idy] * d.nx +
-                                            lny * d.cols_before[idx]);
-  return base + i + lnx * (j + lny * z);
+                                            (long long)lny * d.cols_before[idx]);
+  return base + i + (long long)lnx * (j + (long long)lny * z);
 }
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kPackThreads)
 pack_columns_kernel(const float *__restrict__ global, Decomp d, float *__restrict__ send) {
-  const long long n = (long long)d.nx * d.ny * d.nz;
-  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n;
-       e += (long long)gridDim.x * 256) {
-    const int x = (int)(e % d.nx);
-    const long long r = e / d.nx;
-    const int y = (int)(r % d.ny), z = (int)(r / d.ny);
-    send[chunk_pos(d, x, y, z)] = global[e];
-  }
+  const int x = blockIdx.x * kPackThreads + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
+  if (x >= d.nx) return;
+  send[line_pos(d, x, y, z)] = global[((long long)z * d.ny + y) * d.nx + x];
 }
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kPackThreads)
 unpack_columns_kernel(const float *__restrict__ recv, Decomp d, float *__restrict__ global) {
-  const long long n = (long long)d.nx * d.ny * d.nz;
-  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n;
-       e += (long long)gridDim.x * 256) {
-    const int x = (int)(e % d.nx);
-    const long long r = e / d.nx;
-    const int y = (int)(r % d.ny), z = (int)(r / d.ny);
-    global[e] = recv[chunk_pos(d, x, y, z)];
-  }
+  const int x = blockIdx.x * kPackThreads + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
+  if (x >= d.nx) return;
+  global[((long long)z * d.ny + y) * d.nx + x] = recv[line_pos(d, x, y, z)];
 }
 
 // tmp3d = sgemv('n', n2d*nz_ph, k, 1.0/(g*k), ph, ., x = 1, 0.0) in the reference BLAS
@@ -131,7 +126,9 @@ hipError_t launch_pack_columns(hipStream_t s, const float *global, const Decomp 
                                float *send) {
   const long long n = (long long)d.nx * d.ny * d.nz;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(pack_columns_kernel, grid_for(n), dim3(256), 0, s, global, d, send);
+  if (d.ny > 65535 || d.nz > 65535) return hipErrorInvalidValue;
+  const dim3 grid((d.nx + kPackThreads - 1) / kPackThreads, d.ny, d.nz);
+  hipLaunchKernelGGL(pack_columns_kernel, grid, dim3(kPackThreads), 0, s, global, d, send);
   return hipGetLastError();
 }
 
@@ -139,7 +136,9 @@ hipError_t launch_unpack_columns(hipStream_t s, const float *recv, const Decomp 
                                  float *global) {
   const long long n = (long long)d.nx * d.ny * d.nz;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(unpack_columns_kernel, grid_for(n), dim3(256), 0, s, recv, d, global);
+  if (d.ny > 65535 || d.nz > 65535) return hipErrorInvalidValue;
+  const dim3 grid((d.nx + kPackThreads - 1) / kPackThreads, d.ny, d.nz);
+  hipLaunchKernelGGL(unpack_columns_kernel, grid, dim3(kPackThreads), 0, s, recv, d, global);
   return hipGetLastError();
 }
 

@@ -213,6 +213,9 @@ class Transposer:
             if src == self.rank:
                 f = fields[m]
                 assert f.is_contiguous() and tuple(f.shape) == (nz, gy, gx), (m, tuple(f.shape))
+                if self.world == 1:  # the one chunk is this rank's slab: pack straight into it
+                    self.core.pack_columns(f, gx, gy, nz, self.dec.px, self.dec.py, var[m].view(-1))
+                    continue
                 packed = torch.empty(gx * gy * nz, dtype=torch.float32, device=self.device)
                 self.core.pack_columns(f, gx, gy, nz, self.dec.px, self.dec.py, packed)
                 keep.append(packed)
@@ -239,7 +242,9 @@ class Transposer:
         sends, recvs, packed = [], [], {}
         for m in range(k):
             dst = self.owner(m)
-            if dst == self.rank:
+            if dst == self.rank and self.world == 1:  # unpack straight from the slab (below)
+                packed[m] = var[m].reshape(-1)
+            elif dst == self.rank:
                 buf = torch.empty(gx * gy * nz, dtype=torch.float32, device=self.device)
                 packed[m] = buf
                 for s, (off, cnt) in enumerate(chunks):
