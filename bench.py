@@ -562,6 +562,30 @@ def distinct_devices(world, dev):
     return len({int(v.item()) for v in out})
 
 
+class Stage:
+    """The part of the run in progress, for the error line a failure prints (CWBL_BENCH_FAIL_AT
+    = <stage name> raises there: the tests' failure injection)."""
+
+    def __init__(self):
+        self.name = "setup"
+
+    def __call__(self, name):
+        self.name = name
+        if os.environ.get("CWBL_BENCH_FAIL_AT") == name:
+            raise RuntimeError(f"injected failure at stage {name!r} (CWBL_BENCH_FAIL_AT)")
+
+
+def error_line(args, rank, world, stage, exc):
+    """The JSON line of a run that failed: the contract's keys with value null, the exception
+    and the stage it was raised in (a first RCCL run that fails still reports)."""
+    return {"metric": METRIC, "value": None, "unit": "grid-points/s", "n_gpus": args.gpus,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": None,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic", "config": {"workload": args.config, "ranks": world},
+            "roofline": None, "cpu_baseline": None,
+            "error": repr(exc), "stage": stage.name, "rank": rank}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -584,32 +608,51 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    backend = os.environ.get("CWBL_DIST_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()  # (does not initialise HIP on this image)
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to time "
               f"{world} rank(s) as {args.gpus} GPU(s)", file=sys.stderr, flush=True)
         sys.exit(2)
+    stage = Stage()
+    try:
+        run(args, rank, world, stage)
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        traceback.print_exc()
+        print(f"bench.py rank {rank}: failed in stage {stage.name}: {e!r}", file=sys.stderr,
+              flush=True)
+        if rank == 0:
+            print(json.dumps(error_line(args, rank, world, stage, e)), flush=True)
+        sys.exit(1)
+
+
+def run(args, rank, world, stage):
+    stage("device")
+    backend = os.environ.get("CWBL_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()  # (does not initialise HIP on this image)
     if world > 1 and backend == "nccl" and ndev < world:
-        print(f"bench.py: {world} ranks need {world} distinct GPUs with RCCL, {ndev} visible "
-              f"(CWBL_DIST_BACKEND=gloo rehearses several ranks on one GPU)",
-              file=sys.stderr, flush=True)
-        sys.exit(2)
+        raise RuntimeError(f"{world} ranks need {world} distinct GPUs with RCCL, {ndev} visible "
+                           f"(CWBL_DIST_BACKEND=gloo rehearses several ranks on one GPU)")
     # (gloo rehearsal only: ranks share the visible GPUs modulo their count)
     local = int(os.environ.get("LOCAL_RANK", 0)) % max(ndev, 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        # RCCL over xGMI; CWBL_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU
+        stage("process_group")
+        import datetime
+        # RCCL over xGMI; CWBL_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU.  A
+        # bounded timeout: a rank that dies leaves the others an exception, not a hang
+        tmo = datetime.timedelta(minutes=10)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     n_dev = distinct_devices(world, dev)
 
+    stage("synthesis")
     w = synth.make(args.config, shard=(rank, world) if world > 1 else None)
     k = w.k
     # ---- observation set: packed on rank 0 (obs-set wire format), broadcast over RCCL --------
+    stage("obs_broadcast")
     n = w.obs.shape[0]
     types = [dict(family=1, type_id=w.radar_type, xyz=w.obs_xyz, obs=w.obs, hdxb=w.hdxb)]
     bcast_ms = 0.0
@@ -623,6 +666,7 @@ def main():
     else:
         _, types = cdist.unpack_obs_set(torch.from_numpy(cdist.pack_obs_set(types, k)).to(dev))
     # ---- slab in HBM ---------------------------------------------------------------------------
+    stage("core_init")
     x, y, alt = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt))
     var = torch.from_numpy(w.var).to(dev)
     torch.cuda.synchronize()
@@ -631,9 +675,11 @@ def main():
     core.set_obs(cdist.builder_from(types, abi.MEM_DEVICE).build())
     slab = abi.make_slab(x, y, alt, var, memory=abi.MEM_DEVICE)
 
+    stage("warmup")
     for _ in range(args.warmup):
         core.analyze_var(w.vp, slab)
     core.set_kernel_timing(os.environ.get("CWBL_BENCH_KT", "1") != "0")
+    stage("timed")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -642,12 +688,14 @@ def main():
     for _ in range(args.steps):
         stats.append(core.analyze_var(w.vp, slab))
     torch.cuda.synchronize()
+    t_rank = time.perf_counter() - t0  # this rank's own analysis time (load balance)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ktimes = core.kernel_times()
     core.set_kernel_timing(False)
 
+    stage("reduce")
     pts_local = sum(s.points for s in stats)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -655,8 +703,20 @@ def main():
         p = torch.tensor([pts_local], dtype=torch.float64, device=dev)
         dist.all_reduce(p, op=dist.ReduceOp.SUM)
         elapsed, pts_total = float(t.item()), float(p.item())
+        tr_ = torch.tensor([t_rank / args.steps * 1e3, float(pts_local) / args.steps],
+                           dtype=torch.float64, device=dev)
+        allr = [torch.zeros_like(tr_) for _ in range(world)]
+        dist.all_gather(allr, tr_)
+        rank_ms = [float(v[0]) for v in allr]
+        rank_pts = [int(v[1]) for v in allr]
     else:
         pts_total = float(pts_local)
+        rank_ms, rank_pts = [t_rank / args.steps * 1e3], [int(pts_local / args.steps)]
+    per_rank = {"ms_per_step": rank_ms, "points_per_step": rank_pts,
+                "min_ms": min(rank_ms), "max_ms": max(rank_ms),
+                "imbalance": max(rank_ms) / min(rank_ms) if min(rank_ms) > 0 else None,
+                "note": "each rank's own wall time of the timed steps (before the closing "
+                        "barrier); `value` uses the max over ranks"}
 
     def guarded(fn, *a, **kw):
         # a detail leg that fails is reported in `detail`, never at the cost of the JSON line
@@ -667,6 +727,7 @@ def main():
                   flush=True)
             return {"error": repr(e)}
 
+    stage("detail")
     tr_detail = None if args.no_transposes else guarded(time_transposes, core, w, k, rank,
                                                         world, dev)
     cycle = None if args.no_cycle else guarded(time_cycle, core, w, rank, world, dev, x, y, alt,
@@ -688,13 +749,15 @@ def main():
                 "pinned": guarded(time_host_memory, w, local, steps=3, warmup=1, pinned=True)}
         core = abi.Core(k, device=local)  # (finalised below)
 
+    stage("report")
     if rank == 0:
-        jacobi = os.environ.get("CWBL_SOLVER") == "jacobi"
         solved = sum(s.solved for s in stats)
         nobs_sum = sum(s.nobs_sum for s in stats)
         ms_solve = sum(s.ms_solve for s in stats)
         ms_search = sum(s.ms_search for s in stats)
         roof, per_kernel = roofline_block(ktimes, k, solved, nobs_sum, ms_solve, args.config)
+        hm = legs.get("host_memory") or {}
+        pageable = hm.get("pageable") or {}
         out = {
             "metric": METRIC,
             "value": pts_total / elapsed,
@@ -717,24 +780,28 @@ def main():
                 "n_obs": n,
                 "mean_p": nobs_sum / max(solved, 1),
                 "ranks": world,
+                "slab": "device-resident: var(nx,ny,nz,0:k-1) in HBM before the timed region, as "
+                        "the device member->column transposes (cwbl/transpose.py) leave it; the "
+                        "PCIe-inclusive rate of a pageable host slab is value_host_pageable",
                 "parallelism": f"column-sharded x{world} (px x py = "
                                f"{'x'.join(map(str, tr_dims(world)))})" + (
                     ", obs-set broadcast over " + ("RCCL" if dist.get_backend() == "nccl"
                                                   else dist.get_backend())
                     if world > 1 else ""),
             },
+            "value_host_pageable": pageable.get("value"),
             "roofline": roof,
             "detail": {
-                "solver": "jacobi" if jacobi else "householder+quadrature",
+                "solver": "householder+quadrature",
+                "per_rank": per_rank,
                 "kernels_rank0": per_kernel,
                 "solved_per_step": solved / args.steps,
                 "ms_solve_per_step": ms_solve / args.steps,
                 "ms_search_per_step": ms_search / args.steps,
                 "ms_prep_per_step": sum(s.ms_prep for s in stats) / args.steps,
-                # Jacobi: sweeps; quadrature: decade of the spectrum bound (rule level)
-                ("max_sweeps" if jacobi else "max_quad_level"): max(s.max_sweeps for s in stats),
-                ("mean_sweeps" if jacobi else "mean_quad_level"):
-                    sum(s.sweeps_sum for s in stats) / max(solved, 1),
+                # decade of the quadrature rule's spectrum bound
+                "max_quad_level": max(s.max_sweeps for s in stats),
+                "mean_quad_level": sum(s.sweeps_sum for s in stats) / max(solved, 1),
                 "nonconverged": sum(s.nonconverged for s in stats),
                 "obs_bcast_ms": bcast_ms,
                 "transposes": tr_detail,

@@ -133,7 +133,15 @@ class HostPool {
     int nt = (int)std::min(15u, hw - 1);  // + the calling thread: at most 16
     if (const char *e = std::getenv("OMP_NUM_THREADS"))
       nt = std::max(0, std::min(nt, std::atoi(e) - 1));
-    for (int i = 0; i < nt; ++i) th_.emplace_back([this] { loop(); });
+    // a new worker starts at the current generation: stop() of an earlier pool raised gen_,
+    // and a worker starting from 0 would run a pass no run() handed out (and decrement
+    // busy_ twice)
+    unsigned long g;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      g = gen_;
+    }
+    for (int i = 0; i < nt; ++i) th_.emplace_back([this, g] { loop(g); });
   }
   void work() {
     for (;;) {
@@ -146,8 +154,7 @@ class HostPool {
       (*fn_)(i);
     }
   }
-  void loop() {
-    unsigned long seen = 0;
+  void loop(unsigned long seen) {
     for (;;) {
       {
         std::unique_lock<std::mutex> lk(mu_);
@@ -204,6 +211,7 @@ struct KTime { long long launches = 0, points = 0; double ms = 0.0; };
 struct State {
   bool inited = false;
   int k = 0, kp = 0, device = 0, wf = 0, q1_mode = 0;
+  int kp_natural = 0;  // smallest compiled KP >= k (kp: the one the options select)
   float norain = -5.0f;
   size_t ws_bytes = size_t(2) << 30;
   hipStream_t stream = nullptr;
@@ -650,6 +658,15 @@ void release_all() {
   S.inited = false;
 }
 
+// k = 17..32: the KP = 40 record path (assembly + four-point solve; the padding rows are
+// the identity and the steps past k - 2 exact no-ops) beats the one-wavefront KP = 24 / 32
+// solves (C2 grid, r2: 91.6 against 134 ms per variable at k = 32; r3: ~75 against 79 / 88
+// at k = 20 / 24); at k <= 16 the one-wavefront solve is faster (68 ms)
+void select_kp() {
+  S.kp = S.kp_natural;
+  if ((S.kp == 24 || S.kp == 32) && S.tq4 && !S.jacobi) S.kp = kTq4KP;
+}
+
 SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps, float rtps_a) {
   SolveConsts c{};
   c.k = S.k;
@@ -741,47 +758,91 @@ int cwbl_init(const cwbl_init_params *p) {
     HIPCHK(S.quad.ensure(tab.size() * sizeof(double2)));
     HIPCHK(hipMemcpy(S.quad.p, tab.data(), tab.size() * sizeof(double2), hipMemcpyHostToDevice));
   }
-  const char *solver = std::getenv("CWBL_SOLVER");
-  S.jacobi = solver && std::strcmp(solver, "jacobi") == 0;
+  // path options (cwbl_set_option): every one back to its default
+  S.jacobi = false;
   S.tq4 = 1;
-  if (const char *e = std::getenv("CWBL_TQ4")) S.tq4 = std::atoi(e);
-  if (const char *e = std::getenv("CWBL_TQ4_SUB")) S.tq4_sub = std::atoll(e);
+  S.tq4_sub = 0;
   // r4: one stream by default.  With the r3 kernels the two-stream record path measures a
   // tie (C2 58.7-59.2 M pts/s either way), and serial launches keep each
   // kernel's duration its own (the per-kernel timing and the roofline read it).
   S.tq40_streams = false;
-  if (const char *e = std::getenv("CWBL_TQ40_STREAMS")) S.tq40_streams = std::atoi(e) != 0;
   S.big_split = true;
   // (C4 per variable, r3: 32 k points 2.42 s, 16 k 2.47, 64 k 2.41, 96 k 2.39, 128 k 2.39)
   S.big_sub = 98304;
-  {
-    const char *e = std::getenv("CWBL_SEARCH");
-    S.binned = !(e && std::strcmp(e, "tree") == 0);
-  }
-  if (const char *e = std::getenv("CWBL_BIG_SPLIT")) S.big_split = std::atoi(e) != 0;
+  S.binned = true;
   S.pageable_register = true;
-  if (const char *e = std::getenv("CWBL_PAGEABLE")) S.pageable_register = std::strcmp(e, "bounce") != 0;
   S.bin_div = 0;  // 0: by density (bin_div_for)
-  if (const char *e = std::getenv("CWBL_BIN_DIV")) S.bin_div = std::max(1, std::min(8, std::atoi(e)));
-  if (const char *e = std::getenv("CWBL_BIG_SUB")) S.big_sub = std::max(64LL, std::atoll(e));
-  if (const char *e = std::getenv("CWBL_LEAD_DIV")) S.lead_div = std::atoi(e);
+  S.lead_div = 0;
   S.serial_search = false;
 #ifdef CWBL_DEBUG_KNOBS
   if (const char *e = std::getenv("CWBL_DEBUG_SERIAL")) S.serial_search = std::atoi(e) != 0;
 #endif
-  // k = 17..32: the KP = 40 record path (assembly + four-point solve; the padding rows are
-  // the identity and the steps past k - 2 exact no-ops) beats the one-wavefront KP = 24 / 32
-  // solves (C2 grid, r2: 91.6 against 134 ms per variable at k = 32; r3: ~75 against 79 / 88
-  // at k = 20 / 24); at k <= 16 the one-wavefront solve is faster (68 ms)
-  if ((S.kp == 24 || S.kp == 32) && S.tq4 && !S.jacobi) S.kp = kTq4KP;
+  S.kp_natural = kp;
+  select_kp();
   S.max_batch = 160000;
   S.max_batch_set = false;
-  if (const char *e = std::getenv("CWBL_MAX_BATCH")) {
-    S.max_batch = std::max(256LL, std::atoll(e));
-    S.max_batch_set = true;  // an explicit cap is used as given
-  }
   S.inited = true;
   return CWBL_OK;
+}
+
+int cwbl_set_option(int option, long long value) {
+  if (!S.inited) return fail(CWBL_ERR_STATE, "cwbl_set_option before cwbl_init");
+  auto range = [&](long long lo, long long hi) { return value >= lo && value <= hi; };
+  switch (option) {
+    case CWBL_OPT_SOLVER:
+      if (!range(0, 1)) break;
+      if (value == 1 && S.kp_natural > kMaxWaveKP)
+        return fail(CWBL_ERR_UNSUPPORTED, "the Jacobi solver supports k <= %d", kMaxWaveKP);
+      S.jacobi = value == 1;
+      select_kp();
+      return CWBL_OK;
+    case CWBL_OPT_SPLIT40:
+      if (!range(0, 1)) break;
+      S.tq4 = (int)value;
+      select_kp();
+      return CWBL_OK;
+    case CWBL_OPT_SPLIT40_BATCH:
+      if (!range(0, 1 << 19)) break;
+      S.tq4_sub = value;
+      return CWBL_OK;
+    case CWBL_OPT_SPLIT40_STREAMS:
+      if (!range(0, 1)) break;
+      S.tq40_streams = value != 0;
+      return CWBL_OK;
+    case CWBL_OPT_SEARCH:
+      if (!range(0, 1)) break;
+      S.binned = value == 0;
+      return CWBL_OK;
+    case CWBL_OPT_BIG_PATH:
+      if (!range(0, 1)) break;
+      S.big_split = value == 1;
+      return CWBL_OK;
+    case CWBL_OPT_BIG_BATCH:
+      if (!range(64, 1LL << 24)) break;
+      S.big_sub = value;
+      return CWBL_OK;
+    case CWBL_OPT_PAGEABLE:
+      if (!range(0, 1)) break;
+      S.pageable_register = value == 0;
+      return CWBL_OK;
+    case CWBL_OPT_BIN_DIV:
+      if (!range(0, 8)) break;
+      S.bin_div = (int)value;
+      return CWBL_OK;
+    case CWBL_OPT_LEAD_DIV:
+      if (!range(0, 1 << 20)) break;
+      S.lead_div = (int)value;
+      return CWBL_OK;
+    case CWBL_OPT_MAX_BATCH:
+      if (value != 0 && !range(256, 1LL << 31)) break;
+      S.max_batch = value ? value : 160000;
+      S.max_batch_set = value != 0;  // an explicit cap is used as given
+      return CWBL_OK;
+    default:
+      return fail(CWBL_ERR_ARG, "cwbl_set_option: unknown option %d", option);
+  }
+  return fail(CWBL_ERR_ARG, "cwbl_set_option: value %lld out of range for option %d", value,
+              option);
 }
 
 int cwbl_set_stream(void *stream) {
@@ -970,9 +1031,16 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       (void)hipGetLastError();
     }
   }
-  struct Unregister {  // on every return path
+  struct Unregister {  // on every return path, once no queued copy can still touch var
     bool on; void *p;
-    ~Unregister() { if (on) (void)hipHostUnregister(p); }
+    ~Unregister() {
+      if (!on) return;
+      (void)hipStreamSynchronize(S.h2d);
+      (void)hipStreamSynchronize(S.d2h);
+      (void)hipStreamSynchronize(S.stream);
+      (void)hipGetLastError();
+      (void)hipHostUnregister(p);
+    }
   } unreg{registered, sl->var};
   if (!host) {
     sd.x = sl->x; sd.y = sl->y; sd.alt = sl->alt; sd.var = sl->var;
@@ -1063,12 +1131,17 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     }
     return CWBL_OK;
   };
-  if (bounce) {
-    const size_t slot_bytes = (size_t)Bc * S.k * 4;
+  if (registered) {  // the page-locked slots are only the fallback's: give them back
     for (int i = 0; i < State::kSlots; ++i) {
-      HIPCHK(S.pin_in[i].ensure(slot_bytes));
-      HIPCHK(S.pin_out[i].ensure(slot_bytes));
+      S.pin_in[i].release();
+      S.pin_out[i].release();
     }
+  }
+  if (bounce) {  // the slots the chosen path uses: whole-slab moves alternate two
+    const size_t slot_bytes = (size_t)Bc * S.k * 4;
+    const int nin = piped ? State::kSlots : 2, nout = piped_back ? State::kSlots : 2;
+    for (int i = 0; i < nin; ++i) HIPCHK(S.pin_in[i].ensure(slot_bytes));
+    for (int i = 0; i < nout; ++i) HIPCHK(S.pin_out[i].ensure(slot_bytes));
     if (!piped)
       if (int rc = bounce_whole(true)) return rc;
   }
@@ -1131,15 +1204,23 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   int nrec = 0;                 // record batches so far
   std::vector<int> rec_done;    // cevent after each record batch's solve (on S.tstream)
   std::vector<int> info_done;   // cevent after each search batch's info reduction
-  // one-stream path: the info of the whole call, reduced once after the last batch (a
-  // reduction kernel per batch cost the C2 step ~0.5 ms); the two-stream record path
-  // alternates two batch-sized buffers, reduced per batch
-  HIPCHK(S.info.ensure((size_t)(conc ? B : std::max<long long>(B, npts)) * sizeof(int2)));
+  // one-stream path: the info of a window of up to kInfoWindow points (the whole call below
+  // that), reduced once per window (a reduction kernel per batch cost the C2 step ~0.5 ms);
+  // the two-stream record path alternates two batch-sized buffers, reduced per batch
+  constexpr long long kInfoWindow = 1LL << 25;  // 256 MB of int2
+  const long long info_cap =
+      conc ? B : std::max<long long>(B, std::min<long long>(npts, kInfoWindow));
+  HIPCHK(S.info.ensure((size_t)info_cap * sizeof(int2)));
   if (conc) HIPCHK(S.info2.ensure((size_t)B * sizeof(int2)));
+  long long win0 = 0;  // first point of the current info window (one stream)
   for (long long bi = 0; bi < nbat; ++bi) {
     const long long g0 = plan[bi].first;
     const int nb = plan[bi].second;
-    int2 *const infob = S.info.as<int2>() + (conc ? 0 : g0);  // this batch's info (one stream)
+    if (!conc && g0 + nb - win0 > info_cap) {  // reduce the window; S.stream orders the reuse
+      HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), (int)(g0 - win0), dst));
+      win0 = g0;
+    }
+    int2 *const infob = S.info.as<int2>() + (conc ? 0 : g0 - win0);  // this batch's info
     int *ncnt = (bi & 1) ? S.nbr_cnt2.as<int>() : S.nbr_cnt.as<int>();
     int *nidx = (bi & 1) ? S.nbr_idx2.as<int>() : S.nbr_idx.as<int>();
     hipEvent_t a, b, b2, cc, dn;
@@ -1339,7 +1420,8 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   }
   if (conc && !info_done.empty())  // everything below follows the last solve and reduction
     HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[info_done.back()], 0));
-  if (!conc && npts > 0) HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), (int)npts, dst));
+  if (!conc && npts > win0)
+    HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), (int)(npts - win0), dst));
   if (vp->tune_q) {  // letkf_driver's Q species post-step (:253-278), on the resident slab
     hipEvent_t a, b;
     HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b));

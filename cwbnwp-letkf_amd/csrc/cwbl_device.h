@@ -824,7 +824,7 @@ __device__ __forceinline__ void assemble_point_mfma(
           }
           if constexpr (!L::YO_ROW) fy[b] = ch.yo[4 * g + kk];
         };
-        const int nl = c.debug_stop == 11 ? 0 : nsl;
+        const int nl = CWBL_DBG_STOP(c) == 11 ? 0 : nsl;
         if (nl > 0) load(0, 0);
 #pragma unroll
         for (int g = 0; g < CHUNK / 4; ++g) {

@@ -95,6 +95,15 @@ struct SolveConsts {
   int   debug_steps;          // CWBL_DEBUG_TQ_STEPS: > 0 runs only that many Householder steps
                               // in solve_tq_big_kernel (timing ablation only)
 };
+// The timing-ablation exits read debug_stop / debug_steps only in `make DEBUG_KNOBS=1`
+// builds; in the release library they are the constant 0 and the branches compile away.
+#ifdef CWBL_DEBUG_KNOBS
+#define CWBL_DBG_STOP(c) ((c).debug_stop)
+#define CWBL_DBG_STEPS(c) ((c).debug_steps)
+#else
+#define CWBL_DBG_STOP(c) 0
+#define CWBL_DBG_STEPS(c) 0
+#endif
 
 // Inverse-square-root quadrature of the tq kernels (quad_tables.cpp): level L = 1..kQuadLevels
 // covers spectrum bounds with max/min <= 10^L.  The one-wavefront kernels run kQuadNodes nodes

@@ -152,7 +152,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
       }
       return;
     }
-    if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the rest
+    if (CWBL_DBG_STOP(c) == 1) {  // timing ablation: keep the assembly live, skip the rest
       if (lane == 0 && info) info[gi] = make_int2(ptot, (int)(acc[0][0] + b1acc));
       return;
     }
@@ -171,7 +171,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
       }
       return;
     }
-    if (c.debug_stop == 1) {
+    if (CWBL_DBG_STOP(c) == 1) {
       double t = b1acc;
 #pragma unroll
       for (int q = 0; q < MfmaLayout<KP>::NTL; ++q) t += tile[q][0] + tile[q][3];
@@ -494,7 +494,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
     }
   }
 
-  if (c.debug_stop == 2) {
+  if (CWBL_DBG_STOP(c) == 2) {
     if (lane == 0 && info) info[gi] = make_int2(ptot, (int)(trace + ux + ub));
     return;
   }
@@ -571,7 +571,7 @@ solve_tq_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
   double yl = lane < KP ? Ym[wi] : 0.0;
   const double d = wave_sum_dpp(lane < KP ? sm.tq[lane][2] * zl : 0.0);  // u1 . T^-1 u2
 
-  if (c.debug_stop == 3) {
+  if (CWBL_DBG_STOP(c) == 3) {
     if (lane == 0 && info) info[gi] = make_int2(ptot, (int)d);
     return;
   }
@@ -750,7 +750,7 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
           e[b][2] = dc[ia];
           e[b][3] = dc[ib];
         };
-        const int nl = c.debug_stop == 11 ? 0 : nsl;
+        const int nl = CWBL_DBG_STOP(c) == 11 ? 0 : nsl;
         if (nl > 0) load(0, 0);
 #pragma unroll
         for (int g = 0; g < kTqChunk / 4; ++g) {
@@ -774,7 +774,7 @@ assemble_record_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDe
       RecordSide{sr});
   if (lane == 0) info[gi] = make_int2(ptot, 0);  // p = 0: the solve leaves var unchanged
   if (ptot == 0) return;
-  if (c.debug_stop == 1) {  // timing ablation: keep the assembly live, skip the record
+  if (CWBL_DBG_STOP(c) == 1) {  // timing ablation: keep the assembly live, skip the record
     const double t = t0[0] + t1[1] + t2[2] + st[0] + st[3] + cn;
     if (lane == 0) info[gi] = make_int2(ptot, (int)t);
     return;

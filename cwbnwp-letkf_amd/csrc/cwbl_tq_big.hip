@@ -218,7 +218,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     auto mfma_chunk = [&](int nsl, const CC &cb) {
       // (software-pipelining the group loop, group g + 1's operand reads before group g's
       // MFMAs, measured no faster: 2.52 s per C4 variable either way)
-      for (int s0 = 0; s0 < (c.debug_stop == 12 ? 0 : nsl); s0 += 4) {
+      for (int s0 = 0; s0 < (CWBL_DBG_STOP(c) == 12 ? 0 : nsl); s0 += 4) {
         const float *ys = cb.yb[s0 + kk];
         const double a = (double)ys[offAx], b = (double)ys[offBx];
 #pragma unroll
@@ -312,7 +312,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     return;
   }
 
-  if (c.debug_stop == 1 || c.debug_stop == 12) {  // timing ablation: assembly only
+  if (CWBL_DBG_STOP(c) == 1 || CWBL_DBG_STOP(c) == 12) {  // timing ablation: assembly only
     double t = b1acc;
 #pragma unroll
     for (int it = 0; it < NBL; ++it) t += acc[it][0] + acc[it][15];
@@ -389,7 +389,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   double trace = 0.0;
   static_assert(HS == 0 || (!ASSEMBLED && HS % 4 == 0 && HS + 4 <= KP), "hand-off step");
   // (k > HS + 2 on the split path: every hand-off step is a full step)
-  const int jend = HS > 0 ? HS : c.debug_steps > 0 ? min(k, c.debug_steps) : k;
+  const int jend = HS > 0 ? HS : CWBL_DBG_STEPS(c) > 0 ? min(k, CWBL_DBG_STEPS(c)) : k;
   for (int j = 0; j < jend; ++j) {
     const int J = j >> 2, qj = j & 3;
     // The previous full step read col only before its four later barriers, so only the
@@ -580,7 +580,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     }
   }
 
-  if (c.debug_stop == 2) {
+  if (CWBL_DBG_STOP(c) == 2) {
     if (tid == 0 && info) info[gi] = make_int2(ptot, (int)(trace + ux + ub));
     return;
   }
@@ -665,7 +665,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   double dsum = tid < KP ? sm.tq[tid][2] * zl : 0.0, z5 = 0.0, z6 = 0.0, z7 = 0.0;
   bsum4(dsum, z5, z6, z7);
   const double d = dsum;  // wbar . x' = u1 . T^-1 u2
-  if (c.debug_stop == 3) {
+  if (CWBL_DBG_STOP(c) == 3) {
     if (tid == 0 && info) info[gi] = make_int2(ptot, (int)d);
     return;
   }

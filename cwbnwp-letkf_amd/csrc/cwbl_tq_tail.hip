@@ -245,7 +245,7 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   sm.tq[J0 + l][2] = u1t;
   sm.tq[J0 + l][3] = u2t;
   __syncthreads();
-  if (c.debug_stop == 2) {  // timing ablation: stop after the tridiagonalisation
+  if (CWBL_DBG_STOP(c) == 2) {  // timing ablation: stop after the tridiagonalisation
     if (l == 0) info[gi] = make_int2(ptot, (int)(trace + u1t + u2t));
     return;
   }
@@ -332,7 +332,7 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   double y0 = mem0 ? sm.Ym[w0] : 0.0, y1 = sm.Ym[w1];
   const double d = wave_sum_dpp(fma(mem0 ? sm.tq[l][2] : 0.0, sm.Zm[w0],
                                     sm.tq[J0 + l][2] * sm.Zm[w1]));
-  if (c.debug_stop == 3) {  // timing ablation: stop after the quadrature
+  if (CWBL_DBG_STOP(c) == 3) {  // timing ablation: stop after the quadrature
     if (l == 0) info[gi] = make_int2(ptot, (int)(d + y0 + y1));
     return;
   }

@@ -25,6 +25,14 @@ Q1_REPLICATE, Q1_PER_TYPE = 0, 1
 #: (module_letkf_core.f90:349-417)
 GTS_NVAR = {GTS_SOUND: 4, GTS_SYNOP: 5, GTS_GPSPW: 1, GTS_METAR: 5, GTS_SHIPS: 5}
 
+#: cwbl_set_option options (include/cwb_letkf_core.h)
+OPT_SOLVER, OPT_SPLIT40, OPT_SPLIT40_BATCH, OPT_SPLIT40_STREAMS, OPT_SEARCH = 1, 2, 3, 4, 5
+OPT_BIG_PATH, OPT_BIG_BATCH, OPT_PAGEABLE, OPT_BIN_DIV, OPT_LEAD_DIV, OPT_MAX_BATCH = 6, 7, 8, 9, 10, 11
+OPTIONS = {"solver": OPT_SOLVER, "split40": OPT_SPLIT40, "split40_batch": OPT_SPLIT40_BATCH,
+           "split40_streams": OPT_SPLIT40_STREAMS, "search": OPT_SEARCH,
+           "big_path": OPT_BIG_PATH, "big_batch": OPT_BIG_BATCH, "pageable": OPT_PAGEABLE,
+           "bin_div": OPT_BIN_DIV, "lead_div": OPT_LEAD_DIV, "max_batch": OPT_MAX_BATCH}
+
 ERRORS = {1: "CWBL_ERR_ARG", 2: "CWBL_ERR_STATE", 3: "CWBL_ERR_NO_DEVICE", 4: "CWBL_ERR_HIP",
           5: "CWBL_ERR_UNSUPPORTED", 6: "CWBL_ERR_OOM"}
 
@@ -92,7 +100,7 @@ class KernelTime(C.Structure):
 EXPORTS = ["cwbl_init", "cwbl_set_stream", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch", "cwbl_search",
            "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
            "cwbl_member_sum", "cwbl_scale", "cwbl_set_kernel_timing", "cwbl_kernel_times",
-           "cwbl_finalize", "cwbl_last_error", "cwbl_abi_version"]
+           "cwbl_set_option", "cwbl_finalize", "cwbl_last_error", "cwbl_abi_version"]
 
 
 def _ptr(a):
@@ -268,13 +276,14 @@ def load_library(path=None):
     lib.cwbl_scale.argtypes = [vp, C.c_longlong, C.c_float]
     lib.cwbl_set_kernel_timing.argtypes = [C.c_int]
     lib.cwbl_kernel_times.argtypes = [C.POINTER(KernelTime), C.c_int, C.POINTER(C.c_int)]
+    lib.cwbl_set_option.argtypes = [C.c_int, C.c_longlong]
     lib.cwbl_finalize.argtypes = []
     lib.cwbl_last_error.restype = cp
     lib.cwbl_abi_version.restype = C.c_int
     for fn in ("cwbl_init", "cwbl_set_stream", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch",
                "cwbl_search", "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
                "cwbl_member_sum", "cwbl_scale", "cwbl_set_kernel_timing", "cwbl_kernel_times",
-               "cwbl_finalize"):
+               "cwbl_set_option", "cwbl_finalize"):
         getattr(lib, fn).restype = C.c_int
     return lib
 
@@ -288,13 +297,21 @@ class Core:
     reference's module state)."""
 
     def __init__(self, nmember, device=-1, weight_function=0, norain_value=-5.0,
-                 q1_mode=Q1_REPLICATE, workspace_bytes=0, lib=None):
+                 q1_mode=Q1_REPLICATE, workspace_bytes=0, lib=None, options=None):
+        """options: {name: value} of cwbl_set_option (OPTIONS), applied after cwbl_init."""
         self.lib = lib or load_library()
         if self.lib.cwbl_abi_version() != ABI_VERSION:
             raise CwblError("ABI version mismatch")
         self.k = nmember
         self._check(self.lib.cwbl_init(C.byref(InitParams(
             nmember, device, weight_function, norain_value, q1_mode, 0, workspace_bytes))))
+        for name, value in (options or {}).items():
+            self.set_option(name, value)
+
+    def set_option(self, name, value):
+        """cwbl_set_option by name ("solver", "split40", ..., OPTIONS) or number."""
+        opt = OPTIONS[name] if isinstance(name, str) else int(name)
+        self._check(self.lib.cwbl_set_option(opt, int(value)))
 
     def _check(self, rc):
         if rc != 0:

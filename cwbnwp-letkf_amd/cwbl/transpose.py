@@ -156,9 +156,7 @@ class Transposer:
         mine = self.owned()
         shapes = [tuple(t.shape) for t in fields[mine[0]]] if mine else []
         if self.world > 1:  # every rank needs the layout (a rank may own no member)
-            box = [shapes]
-            dist.broadcast_object_list(box, src=self._peer(self.owner(0)), group=self.group)
-            shapes = box[0]
+            shapes = self._bcast_shapes(shapes, self.owner(0))
         sizes = [int(np.prod(sh)) for sh in shapes]
         n = int(sum(sizes))
         packed = torch.empty((max(len(mine), 1), n), dtype=torch.float32, device=self.device)
@@ -189,6 +187,29 @@ class Transposer:
             out.append(total[off:off + sz].reshape(sh))
             off += sz
         return out
+
+    MAX_FIELDS, MAX_DIMS = 64, 4
+
+    def _bcast_shapes(self, shapes, src):
+        """The field shapes of rank `src` to every rank as one fixed-size int64 tensor
+        (count, then per field ndim and up to MAX_DIMS extents): no pickled object on the data
+        path."""
+        torch, dist = self.torch, self.dist
+        w = 1 + self.MAX_DIMS
+        buf = torch.zeros(1 + self.MAX_FIELDS * w, dtype=torch.int64)
+        if self.rank == src:
+            if len(shapes) > self.MAX_FIELDS or any(len(sh) > self.MAX_DIMS for sh in shapes):
+                raise ValueError(f"write_mean: at most {self.MAX_FIELDS} fields of <= "
+                                 f"{self.MAX_DIMS} dimensions")
+            buf[0] = len(shapes)
+            for i, sh in enumerate(shapes):
+                buf[1 + i * w] = len(sh)
+                for d, e in enumerate(sh):
+                    buf[2 + i * w + d] = int(e)
+        t = buf.to(self.device) if self.backend == "nccl" else buf
+        dist.broadcast(t, src=self._peer(src), group=self.group)
+        v = t.cpu().tolist()
+        return [tuple(v[2 + i * w: 2 + i * w + v[1 + i * w]]) for i in range(v[0])]
 
     def _member_sum(self, packed, n, nm, out):
         self.core.member_sum(packed, n, nm, out)

@@ -75,7 +75,7 @@ module letkf_core_gpu
 
     public :: cwbl_init, cwbl_set_obs, cwbl_analyze_var, cwbl_solve_batch, cwbl_search, &
               cwbl_pack_columns, cwbl_unpack_columns, cwbl_vcoord_mean, &
-              cwbl_member_sum, cwbl_scale, cwbl_set_stream, &
+              cwbl_member_sum, cwbl_scale, cwbl_set_stream, cwbl_set_option, &
               cwbl_finalize, cwbl_abi_version, cwbl_error, cwbl_check
     ! host obs ingest (include/cwb_letkf_ingest.h); file names and varname are passed as
     ! trim(name)//c_null_char
@@ -234,6 +234,13 @@ module letkf_core_gpu
             real(c_float),        intent(out) :: buf(*)
             integer(c_long_long), value       :: cap_words
         end function cwbl_ingest_pack_wire
+
+        ! path options (A/B measurement; include/cwb_letkf_core.h CWBL_OPT_*), after cwbl_init
+        integer(c_int) function cwbl_set_option(option, val) bind(C, name='cwbl_set_option')
+            import :: c_int, c_long_long
+            integer(c_int),       value :: option
+            integer(c_long_long), value :: val
+        end function cwbl_set_option
 
         integer(c_int) function cwbl_finalize() bind(C, name='cwbl_finalize')
             import :: c_int

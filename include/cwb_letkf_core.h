@@ -276,6 +276,33 @@ typedef struct cwbl_kernel_time {
 int         cwbl_set_kernel_timing(int enable);
 int         cwbl_kernel_times(cwbl_kernel_time *out, int cap, int *n);
 
+/* ---- path options (no reference counterpart) ---------------------------------------------
+ * The library reads no environment variable but OMP_NUM_THREADS (which caps the host threads
+ * of the pageable-slab bounce fallback).  The alternative kernel paths and batch sizes below
+ * are kept for A/B measurement and for the parity tests that compare one path with another;
+ * they are set after cwbl_init, which resets every option to its default.  A value outside
+ * an option's range returns CWBL_ERR_ARG.  No option changes a result beyond the fp64
+ * summation order of the solve (every path meets the same parity bar). */
+enum {
+  CWBL_OPT_SOLVER = 1,         /* 0 Householder + quadrature (default); 1 the Jacobi
+                                * eigensolver (k <= 64, analysis and solve_batch) */
+  CWBL_OPT_SPLIT40 = 2,        /* k = 17..40: 1 assembly record + four-point solve (default);
+                                * 0 the one-wavefront kernel */
+  CWBL_OPT_SPLIT40_BATCH = 3,  /* points per record sub-batch of that path (0 = search batch) */
+  CWBL_OPT_SPLIT40_STREAMS = 4,/* 1: its four-point solve on a second stream (default 0) */
+  CWBL_OPT_SEARCH = 5,         /* 0 uniform bins + tree for truncated lists (default); 1 the
+                                * k-d tree walk for every point */
+  CWBL_OPT_BIG_PATH = 6,       /* k = 65..128: 1 256-thread hand-off + one-wave tail (default);
+                                * 0 one 256-thread kernel */
+  CWBL_OPT_BIG_BATCH = 7,      /* points per k > 64 sub-batch (>= 64; default 98 304) */
+  CWBL_OPT_PAGEABLE = 8,       /* pageable host slab: 0 page-lock in place (default); 1 bounce
+                                * through the library's page-locked slots */
+  CWBL_OPT_BIN_DIV = 9,        /* search bin side = radius / value, 1..8 (0 = by obs density) */
+  CWBL_OPT_LEAD_DIV = 10,      /* first search batch = points / value (0 = off, default) */
+  CWBL_OPT_MAX_BATCH = 11      /* points per search batch, >= 256 (0 = automatic, default) */
+};
+int         cwbl_set_option(int option, long long value);
+
 int         cwbl_finalize(void);
 const char *cwbl_last_error(void);
 int         cwbl_abi_version(void);

@@ -34,15 +34,13 @@ def core(k, wf=0, norain=-5.0, q1=abi.Q1_REPLICATE):
 
 @pytest.mark.parametrize("k,solver", [(8, "tq"), (40, "tq"), (64, "tq"), (128, "tq"),
                                       (8, "jacobi"), (40, "jacobi"), (64, "jacobi")])
-def test_solve_batch_matches_reference(k, solver, monkeypatch):
+def test_solve_batch_matches_reference(k, solver):
     """G1 through cwbl_solve_batch with the eigenvalue output: increments within 1e-6 and
     dsyevd's ascending eigenvalues within 1e-12 at every k.  Default: the tq kernels' T and
-    bisection (cwbl_eig.hip); CWBL_SOLVER=jacobi (k <= 64): the Jacobi eigensolver."""
+    bisection (cwbl_eig.hip); option solver = 1 (k <= 64): the Jacobi eigensolver."""
     g = golden(f"solve_k{k}.npz")
-    if solver == "jacobi":
-        monkeypatch.setenv("CWBL_SOLVER", "jacobi")
     _cores.clear()
-    c = abi.Core(k, device=0)
+    c = abi.Core(k, device=0, options={"solver": int(solver == "jacobi")})
     col = g["col_off"]
     # group points that share the solve parameters
     keys = list(zip(g["multi_infl"], g["use_rtpp"], g["use_rtps"], g["rtpp_alpha"], g["rtps_alpha"]))
@@ -251,20 +249,19 @@ def test_synthetic_c2_subdomain_vs_oracle():
 
 
 @pytest.mark.parametrize("k", [17, 20, 24, 25, 32, 33, 36, 40])
-def test_split_kp40_path_vs_one_kernel_and_oracle(k, monkeypatch):
+def test_split_kp40_path_vs_one_kernel_and_oracle(k):
     """The KP = 40 slab path runs split by default (assemble_record_kernel writes A and Yb d,
-    solve_tq40_kernel runs the whole tridiagonalisation four points per wavefront, CWBL_TQ4=1).
+    solve_tq40_kernel runs the whole tridiagonalisation four points per wavefront, split40 = 1).
     k < 40 exercises the identity padding (the no-op steps past
-    k - 2); k = 17..32 run at KP = 40 too (their one-kernel paths, CWBL_TQ4=0, are KP = 24, 32).
-    Both against the one-kernel path (CWBL_TQ4=0) and the oracle on a 30x30x50 C2-shaped
+    k - 2); k = 17..32 run at KP = 40 too (their one-kernel paths, split40 = 0, are KP = 24, 32).
+    Both against the one-kernel path (split40 = 0) and the oracle on a 30x30x50 C2-shaped
     grid."""
     import ctypes as C
     w = _radar_case_scaled(0.1, k=k)
     out = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("CWBL_TQ4", mode)
         _cores.clear()
-        c = abi.Core(w.k, device=0)
+        c = abi.Core(w.k, device=0, options={"split40": int(mode)})
         c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
         var = w.var.copy()
         st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
@@ -316,7 +313,7 @@ def test_two_chunk_staging_at_sparse_densities(n_obs):
     assert (dn <= tol).all(), int(np.argmax(dn - tol))
 
 
-def test_split_kp40_ragged_record_batches(monkeypatch):
+def test_split_kp40_ragged_record_batches():
     """Record sub-batches whose point count is not a multiple of four: the last wave of
     solve_tq40_kernel has lanes past the batch, which must not disturb a live point's record
     (they work on a spare record).  31x29x7 = 6293 points in sub-batches of 512 (the last has
@@ -327,9 +324,8 @@ def test_split_kp40_ragged_record_batches(monkeypatch):
     assert w.points % 4 == 1
     out = {}
     for sub in ("512", "0"):
-        monkeypatch.setenv("CWBL_TQ4_SUB", sub)
         _cores.clear()
-        c = abi.Core(w.k, device=0)
+        c = abi.Core(w.k, device=0, options={"split40_batch": int(sub)})
         c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
         var = w.var.copy()
         st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
@@ -385,34 +381,73 @@ def test_c2_full_size_properties():
     assert rel <= INCR_TOL, rel
 
 
-def test_batch_plan_does_not_change_the_analysis(monkeypatch):
+@pytest.mark.timeout(900)
+def test_c2_full_grid_vs_oracle():
+    """The headline configuration end to end against the oracle on EVERY point: the HIP core
+    on the whole 300x300x50 C2 grid (k = 40, 22 500 obs, mean p ~216) and the C oracle's
+    letkf_driver loop (module_letkf_core.f90:209-240) on the same 4.5 M points with all the
+    host cores the job may use; whole-grid increments within 1e-6 relative RMS, the solved
+    and accepted-obs counts equal, and per column block of 30x30 columns within 1e-6 as well
+    (so that an error confined to a region cannot hide in the whole-grid mean)."""
+    import ctypes as C
+    from bench import baseline_procs
+    from cwbl import synth
+    w = synth.make("c2")
+    c = core(w.k)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    var = w.var.copy()
+    st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+    ref = w.var.copy()
+    ost = abi.Stats()
+    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
+    threads, _ = baseline_procs()
+    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
+                                  C.byref(abi.make_slab(w.x, w.y, w.alt, ref)), threads,
+                                  C.byref(ost))
+    assert rc == 0
+    assert st.solved == ost.solved and st.nobs_sum == ost.nobs_sum
+    assert st.points == w.points == 300 * 300 * 50
+    rel = increment_rel_rms(var, ref, w.var)
+    assert rel <= INCR_TOL, rel
+    worst = 0.0
+    for j0 in range(0, 300, 30):
+        for i0 in range(0, 300, 30):
+            b = (Ellipsis, slice(j0, j0 + 30), slice(i0, i0 + 30))
+            if np.array_equal(ref[b], w.var[b]):
+                continue  # no solved point in the block: must be untouched
+            worst = max(worst, increment_rel_rms(var[b], ref[b], w.var[b]))
+    assert worst <= INCR_TOL, worst
+    untouched = ref == w.var
+    np.testing.assert_array_equal(var[untouched].view(np.uint32), w.var[untouched].view(np.uint32))
+
+
+def test_batch_plan_does_not_change_the_analysis():
     """Points are independent, so the search/solve batch plan (batch cap, short lead batch,
     two list buffers alternating between overlapped searches and solves) must not change
     a single bit of the analysis."""
     from cwbl import synth
     w = synth.make("c2", scale=0.2)
     out = []
-    for env in ({}, {"CWBL_MAX_BATCH": "9000", "CWBL_LEAD_DIV": "8"}):
-        for key in ("CWBL_MAX_BATCH", "CWBL_LEAD_DIV"):
-            monkeypatch.delenv(key, raising=False)
-        for key, val in env.items():
-            monkeypatch.setenv(key, val)
+    for opts in ({}, {"max_batch": 9000, "lead_div": 8}):
         _cores.clear()
-        c = core(w.k)
+        c = abi.Core(w.k, device=0, options=opts)
         c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
         var = w.var.copy()
         c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+        c.finalize()
         out.append(var)
     _cores.clear()
     assert np.isfinite(out[0]).all()
     np.testing.assert_array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
 
 
+@pytest.mark.timeout(600)
 def test_c4_full_size_properties():
     """Full C4 size (300x300x50, k=128, the 256-thread kernel): finite, bitwise reproducible
     run to run (a cross-wave LDS race once showed up only as a few NaN points that moved
     between runs), and the oracle on a column block."""
     import ctypes as C
+    from bench import baseline_procs
     from cwbl import synth
     w = synth.make("c4")
     c = core(w.k)
@@ -425,28 +460,29 @@ def test_c4_full_size_properties():
     var2 = w.var.copy()
     c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var2))
     np.testing.assert_array_equal(var.view(np.uint32), var2.view(np.uint32))
-    j0, i0, nb = 140, 150, 5
+    # the oracle on a 20x20-column block (20 000 points, all 50 levels)
+    j0, i0, nb = 140, 140, 20
     sub = lambda a: np.ascontiguousarray(a[..., j0:j0 + nb, i0:i0 + nb])  # noqa: E731
     ref = sub(w.var).copy()
     ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
     rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
                                   C.byref(abi.make_slab(sub(w.x), sub(w.y), sub(w.alt), ref)),
-                                  16, C.byref(abi.Stats()))
+                                  baseline_procs()[0], C.byref(abi.Stats()))
     assert rc == 0
     rel = increment_rel_rms(sub(var), ref, sub(w.var))
     assert rel <= INCR_TOL, rel
 
 
 @pytest.mark.parametrize("name", ["driver_mixed.npz", "driver_gc_k40.npz"])
-def test_tq_and_jacobi_solvers_agree(name, monkeypatch):
-    """The two solve kernels (eigendecomposition by Jacobi, CWBL_SOLVER=jacobi; and the
+def test_tq_and_jacobi_solvers_agree(name):
+    """The two solve kernels (eigendecomposition by Jacobi, option solver = 1; and the
     default tridiagonalisation + quadrature) give the same analysis to the tolerance."""
     case = DriverCase(name)
     out = {}
     for solver in ("jacobi", "tq"):
-        monkeypatch.setenv("CWBL_SOLVER", solver)
         _cores.clear()
-        c = abi.Core(case.k, device=0, weight_function=case.wf, norain_value=case.norain)
+        c = abi.Core(case.k, device=0, weight_function=case.wf, norain_value=case.norain,
+                     options={"solver": int(solver == "jacobi")})
         c.set_obs(case.obs_set())
         slab, var = case.slab()
         c.analyze_var(case.vp, slab)
@@ -573,12 +609,12 @@ def test_large_ensemble_block_vs_oracle(k):
 
 @pytest.mark.parametrize("k,sparse", [(65, False), (80, True), (96, False), (97, False),
                                       (101, True), (127, False), (128, False), (128, True)])
-def test_split_big_path_vs_one_kernel_and_oracle(k, sparse, monkeypatch):
+def test_split_big_path_vs_one_kernel_and_oracle(k, sparse):
     """The KP = 96 / 128 slab paths run split by default: solve_tq_big_kernel<KP, false,
     KP - 64> (256 threads per point) hands the trailing 64x64 matrix and its reflectors to
     solve_tqb_tail_kernel (one point per wavefront).  k < KP exercises the identity padding;
     the sparse obs set gives points with p < k (rank-deficient Yb Yb^T, exactly-zero
-    reflectors, tau = 0).  Against the one-kernel path (CWBL_BIG_SPLIT=0) on the whole
+    reflectors, tau = 0).  Against the one-kernel path (big_path = 0) on the whole
     30x30x50 grid and the oracle on a 5x5-column block; hand-off batches of 1024 points."""
     import ctypes as C
     from cwbl import synth
@@ -588,12 +624,10 @@ def test_split_big_path_vs_one_kernel_and_oracle(k, sparse, monkeypatch):
         w.obs_xyz = np.ascontiguousarray(w.obs_xyz[keep])
         w.obs = np.ascontiguousarray(w.obs[keep])
         w.hdxb = np.ascontiguousarray(w.hdxb[:, keep])
-    monkeypatch.setenv("CWBL_BIG_SUB", "1024")
     out = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("CWBL_BIG_SPLIT", mode)
         _cores.clear()
-        c = abi.Core(w.k, device=0)
+        c = abi.Core(w.k, device=0, options={"big_batch": 1024, "big_path": int(mode)})
         c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
         var = w.var.copy()
         st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
@@ -691,7 +725,7 @@ def test_large_k_random_batch_vs_oracle(k):
 
 
 @pytest.mark.parametrize("name", ["c2", "c2_far", "c5", "driver_mixed.npz", "driver_c1.npz"])
-def test_binned_search_equals_tree_search(name, monkeypatch):
+def test_binned_search_equals_tree_search(name):
     """The analysis search runs on uniform bins (search_binned_kernel) with the k-d tree as
     the fallback where max_lz truncates (Q4).  The neighbour SETS are identical, so the solved
     points, the accepted-obs counts and the truncation counts must match the tree search's
@@ -701,8 +735,8 @@ def test_binned_search_equals_tree_search(name, monkeypatch):
     from cwbl import synth
     if name.endswith(".npz"):
         case = DriverCase(name)
-        mk = lambda: (abi.Core(case.k, device=0, weight_function=case.wf,  # noqa: E731
-                               norain_value=case.norain), case.obs_set(), case.vp)
+        mk = lambda o: (abi.Core(case.k, device=0, weight_function=case.wf,  # noqa: E731
+                                 norain_value=case.norain, options=o), case.obs_set(), case.vp)
         slabs = lambda: case.slab()  # noqa: E731
         var_in = case.var_in
     else:
@@ -715,7 +749,7 @@ def test_binned_search_equals_tree_search(name, monkeypatch):
                 tp.hclr = tp.hclr / 8.0
         ob = lambda: abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs,  # noqa: E731
                                                     w.hdxb).build()
-        mk = lambda: (abi.Core(w.k, device=0), ob(), w.vp)  # noqa: E731
+        mk = lambda o: (abi.Core(w.k, device=0, options=o), ob(), w.vp)  # noqa: E731
 
         def slabs():
             var = w.var.copy()
@@ -723,9 +757,8 @@ def test_binned_search_equals_tree_search(name, monkeypatch):
         var_in = w.var
     out = {}
     for mode in ("tree", "bins"):
-        monkeypatch.setenv("CWBL_SEARCH", mode)
         _cores.clear()
-        c, obs, vp = mk()
+        c, obs, vp = mk({"search": int(mode == "tree")})
         c.set_obs(obs)
         slab, var = slabs()
         st = c.analyze_var(vp, slab)
@@ -894,26 +927,24 @@ def test_ingested_obs_set_analysis_vs_oracle():
 @pytest.mark.parametrize("tune_q", [0, 1])
 @pytest.mark.parametrize("host", ["pageable", "pageable_bounce", "pinned"])
 @pytest.mark.parametrize("staggered", [False, True])
-def test_pipelined_host_slab_equals_device_slab(tune_q, host, staggered, monkeypatch):
+def test_pipelined_host_slab_equals_device_slab(tune_q, host, staggered):
     """A host-memory slab whose analysed region is the whole horizontal slab moves var batch
     by batch (H2D before each batch's solve on its own stream, D2H behind each batch's last
     solve; with tune_q the copy back waits for the whole slab).  Pageable numpy arrays are
-    page-locked in place for the call (hipHostRegister) or, with CWBL_PAGEABLE=bounce, go
+    page-locked in place for the call (hipHostRegister) or, with option pageable = 1, go
     through the library's page-locked bounce slots (host threads fill and drain them);
     page-locked ones (torch pin_memory) are copied directly.  A staggered slab (ix_lim < nx,
     the U variable's Q2 bounds) moves whole.  Bit-identical to the device-memory call, over
     many batches."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("CWBL_MAX_BATCH", "3000")
-    if host == "pageable_bounce":
-        monkeypatch.setenv("CWBL_PAGEABLE", "bounce")
+    opts = {"max_batch": 3000, "pageable": int(host == "pageable_bounce")}
     pinned = host == "pinned"
     _cores.clear()
     w = _radar_case_scaled(0.1, nz=12)
     vp = w.vp
     vp.tune_q = tune_q
     ix_lim = w.x.shape[1] - 1 if staggered else None
-    c = abi.Core(w.k, device=0)
+    c = abi.Core(w.k, device=0, options=opts)
     c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
     if pinned:
         t = torch.empty(w.var.shape, dtype=torch.float32, pin_memory=True)
@@ -929,3 +960,21 @@ def test_pipelined_host_slab_equals_device_slab(tune_q, host, staggered, monkeyp
     c.finalize()
     assert st.solved > 0
     np.testing.assert_array_equal(hv.view(np.uint32), dv.cpu().numpy().view(np.uint32))
+
+
+def test_set_option_ranges_and_reset():
+    """cwbl_set_option: unknown options and out-of-range values are CWBL_ERR_ARG, the Jacobi
+    solver past k = 64 is CWBL_ERR_UNSUPPORTED, and cwbl_init resets every option (the
+    library reads no environment knob)."""
+    _cores.clear()
+    c = abi.Core(40, device=0)
+    for opt, val in ((99, 0), (abi.OPT_SPLIT40, 2), (abi.OPT_BIG_BATCH, 8),
+                     (abi.OPT_MAX_BATCH, 100), (abi.OPT_BIN_DIV, 9)):
+        with pytest.raises(abi.CwblError, match="CWBL_ERR_ARG"):
+            c.set_option(opt, val)
+    c.set_option("max_batch", 0)
+    c.finalize()
+    c = abi.Core(128, device=0)
+    with pytest.raises(abi.CwblError, match="CWBL_ERR_UNSUPPORTED"):
+        c.set_option("solver", 1)
+    c.finalize()

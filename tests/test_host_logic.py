@@ -144,3 +144,52 @@ def test_baseline_process_count_follows_affinity_and_quota():
     procs, note = bench.baseline_procs()
     assert procs == (n_phys if quota is None else max(1, min(n_phys, int(quota))))
     assert f"{procs} used" in note
+
+
+def _bench_json(stdout):
+    import json
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert lines, stdout
+    return json.loads(lines[-1])
+
+
+def test_bench_failure_still_prints_a_json_line():
+    """A run that fails (here by CWBL_BENCH_FAIL_AT's injection at the first stage; on a
+    first RCCL run it would be process-group init or the obs broadcast) still ends in one
+    parseable JSON line with value null, the exception and the stage it came from."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CWBL_BENCH_FAIL_AT="device")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1, r.stderr[-2000:]
+    d = _bench_json(r.stdout)
+    assert d["value"] is None and d["stage"] == "device" and "injected" in d["error"]
+    assert d["metric"].startswith("analysis grid-points/sec")
+
+
+def test_bench_two_rank_failure_reports_from_rank_0():
+    """The same under torch.distributed.run with two ranks (gloo, CPU): rank 0 prints the
+    error line, the run exits non-zero, and nothing hangs."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, CWBL_BENCH_FAIL_AT="device", CWBL_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr=127.0.0.1",
+                        f"--master-port={port}", os.path.join(repo, "bench.py"), "--gpus", "2",
+                        "--steps", "1"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    d = _bench_json(r.stdout)
+    assert d["value"] is None and d["stage"] == "device" and d["rank"] == 0
+    assert d["config"]["ranks"] == 2
