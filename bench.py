@@ -198,12 +198,19 @@ def cpu_baseline_reference(w, target_s=12.0, procs=None):
 
 def time_transposes(core, w, k, rank, world, dev):
     """One letkf_scatter_grid + letkf_gather_grid of the whole variable (k members of
-    nx x ny x nz fp32) through cwbl/transpose.py: HIP packing + RCCL point-to-point.
-    Members are dealt m % world; max over ranks of one timed pass after one warm-up."""
+    nx x ny x nz fp32) through cwbl/transpose.py: HIP packing + RCCL point-to-point, the
+    owned members held as one stacked tensor (one packing launch per transpose; on one rank
+    the column layout is the member layout and var aliases the fields, no copy).  Members
+    are dealt m % world; max over ranks of one timed pass after one warm-up.  The packing
+    kernels alone are timed as well (pack_members / unpack_members of the owned members
+    into a separate buffer, best of 5): their effective HBM rate, 2 x 4 B per element."""
     from cwbl import transpose as tr
     nx, ny, nz = w.extra["cfg"]["nx"], w.extra["cfg"]["ny"], w.nz
     t = tr.Transposer(core, k, nx, ny, device=dev)
-    fields = {m: torch.randn((nz, ny, nx), device=dev) for m in t.owned()}
+    mine = t.owned()
+    stk = torch.randn((len(mine), nz, ny, nx), device=dev)
+    fields = {m: stk[i] for i, m in enumerate(mine)}
+    ref = stk.clone()
     res = {}
     for it in range(2):
         torch.cuda.synchronize()
@@ -212,19 +219,39 @@ def time_transposes(core, w, k, rank, world, dev):
         t0 = time.perf_counter()
         var = t.scatter_grid(fields, nz)
         t1 = time.perf_counter()
-        back = t.gather_grid(var)
+        back = t.gather_grid(var, out=fields)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         res = {"scatter_ms": (t1 - t0) * 1e3, "gather_ms": (t2 - t1) * 1e3}
-    for m in t.owned():
-        assert torch.equal(back[m], fields[m]), "transpose round trip"
+    for i, m in enumerate(mine):
+        assert torch.equal(back[m], ref[i]), "transpose round trip"
+    n = nx * ny * nz
+    buf = torch.empty((max(len(mine), 1), n), device=dev)
+    px, py = t.dec.px, t.dec.py
+    kern = {}
+    for name, fn in (("pack", lambda: core.pack_members(stk, n, len(mine), nx, ny, nz, px, py, buf, n)),
+                     ("unpack", lambda: core.unpack_members(buf, n, len(mine), nx, ny, nz, px, py, stk, n))):
+        best = None
+        for _ in range(5):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            fn()
+            el = time.perf_counter() - a
+            best = el if best is None else min(best, el)
+        kern[f"{name}_ms"] = best * 1e3
+        kern[f"{name}_gbs"] = 2 * 4 * n * len(mine) / best / 1e9
     if world > 1:
         v = torch.tensor([res["scatter_ms"], res["gather_ms"]], dtype=torch.float64, device=dev)
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         res = {"scatter_ms": float(v[0]), "gather_ms": float(v[1])}
     gb = k * nx * ny * nz * 4 / 1e9
     res.update(variable_gb=gb, px_py=list(tr.dims_create(world)),
-               scatter_gbs=gb / (res["scatter_ms"] * 1e-3), gather_gbs=gb / (res["gather_ms"] * 1e-3))
+               scatter_gbs=gb / max(res["scatter_ms"] * 1e-3, 1e-9),
+               gather_gbs=gb / max(res["gather_ms"] * 1e-3, 1e-9),
+               kernels_rank0=dict(kern, members=len(mine),
+                                  note="one launch over the owned members, host wall time of "
+                                       "the synchronous call (launch + sync included)"),
+               aliased=world == 1)
     return res
 
 
@@ -281,8 +308,9 @@ def time_cycle(core, w, rank, world, dev, x, y, alt, transposes=True):
     for kind, (stg, up) in KINDS.items():
         nzv = 1 if up is None else nz + up
         gx, gy = t.dec.grid(stg)
-        if transposes:
-            fields[kind] = {m: torch.randn((nzv, gy, gx), device=dev) for m in t.owned()}
+        if transposes:  # the owned members' fields as one stacked tensor
+            stk = torch.randn((len(t.owned()), nzv, gy, gx), device=dev)
+            fields[kind] = {m: stk[i] for i, m in enumerate(t.owned())}
         lx, ly = t.local_shape(stg)
         slabs[kind] = (nzv, stg, lx, ly, _kind_slab(kind, x, y, alt, lx, ly),
                        None if transposes else torch.randn((k, nzv, ly, lx), device=dev))

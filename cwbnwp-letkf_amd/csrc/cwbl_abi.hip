@@ -1574,6 +1574,38 @@ int cwbl_unpack_columns(const float *recv, int nx, int ny, int nz, int px, int p
   return CWBL_OK;
 }
 
+int cwbl_pack_members(const float *global, long long gstride, int nm, int nx, int ny, int nz,
+                      int px, int py, float *send, long long sstride) {
+  if (int rc = require_device()) return rc;
+  const long long n = (long long)nx * ny * nz;
+  if (nx < 0 || ny < 0 || nz < 0 || px < 1 || py < 1 || px > kMaxRankDim || py > kMaxRankDim ||
+      nm < 0 || nm > 65535 || (nm > 1 && (gstride < n || sstride < n)) ||
+      (n > 0 && nm > 0 && (!global || !send)))
+    return fail(CWBL_ERR_ARG, "cwbl_pack_members: bad arguments");
+  Decomp d;
+  make_decomp(d, nx, ny, nz, px, py);
+  HIPCHK(order_after_caller());
+  HIPCHK(launch_transpose_columns(S.stream, false, global, gstride, nm, d, send, sstride));
+  HIPCHK(hipStreamSynchronize(S.stream));
+  return CWBL_OK;
+}
+
+int cwbl_unpack_members(const float *recv, long long rstride, int nm, int nx, int ny, int nz,
+                        int px, int py, float *global, long long gstride) {
+  if (int rc = require_device()) return rc;
+  const long long n = (long long)nx * ny * nz;
+  if (nx < 0 || ny < 0 || nz < 0 || px < 1 || py < 1 || px > kMaxRankDim || py > kMaxRankDim ||
+      nm < 0 || nm > 65535 || (nm > 1 && (gstride < n || rstride < n)) ||
+      (n > 0 && nm > 0 && (!global || !recv)))
+    return fail(CWBL_ERR_ARG, "cwbl_unpack_members: bad arguments");
+  Decomp d;
+  make_decomp(d, nx, ny, nz, px, py);
+  HIPCHK(order_after_caller());
+  HIPCHK(launch_transpose_columns(S.stream, true, recv, rstride, nm, d, global, gstride));
+  HIPCHK(hipStreamSynchronize(S.stream));
+  return CWBL_OK;
+}
+
 int cwbl_vcoord_mean(const float *ph, long long n2d, int nz_ph, int k, int stagger, float g,
                      float *alt) {
   if (int rc = require_device()) return rc;

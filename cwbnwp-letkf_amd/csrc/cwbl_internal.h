@@ -162,6 +162,10 @@ hipError_t launch_pack_columns(hipStream_t s, const float *global, const Decomp 
                                float *send);
 hipError_t launch_unpack_columns(hipStream_t s, const float *recv, const Decomp &d,
                                  float *global);
+// nm member fields at once (member i at src + i sstride -> dst + i dstride, in elements)
+hipError_t launch_transpose_columns(hipStream_t s, bool unpack, const float *src,
+                                    long long sstride, int nm, const Decomp &d, float *dst,
+                                    long long dstride);
 hipError_t launch_vcoord_mean(hipStream_t s, const float *ph, long long n2d, int nz_ph, int k,
                               int stagger, float alpha, float *alt);
 hipError_t launch_member_sum(hipStream_t s, const float *fields, long long n, int nm,

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 
 namespace cwbl {
 
@@ -41,33 +42,69 @@ void make_decomp(Decomp &d, int nx, int ny, int nz, int px, int py) {
 }
 
 // Element (x, y, z) of global(nx,ny,nz) goes to its position in the rank-major chunk buffer
-// (line_pos).  One block row per (y, z) line of the field (blockIdx.y = y, blockIdx.z = z), threads along
-// x: the row's rank-grid row and offsets are block-uniform, and a thread does one 32-bit
-// division (x by px) instead of the 64-bit element decomposition (r4: the kernels were
-// integer-division bound at ~0.7 TB/s).
-constexpr int kPackThreads = 128;
-__device__ inline long long line_pos(const Decomp &d, int x, int y, int z) {
-  const int idy = y % d.py, j = y / d.py;   // block-uniform
-  const int lny = cyc_count(d.ny, idy, d.py);
+// (line_pos).  One wavefront per (y, z) line of one member's field (r5: the line index and
+// the member come from the block, four lines per 256-thread block, so there is no 65535 limit
+// on ny or nz), each lane moving four consecutive x: the global side is one 16-B access per
+// lane where the line is 16-B aligned (nx % 4 == 0 and an aligned field), the chunk side four
+// 4-B accesses that a wavefront writes as px contiguous runs.  The row's rank-grid row and
+// offsets are wave-uniform; a lane does one 32-bit division (x by px) per element.
+constexpr int kPackThreads = 256, kPackLines = kPackThreads / 64;
+struct LineMap {  // the chunk-side offsets of one (y, z) line
+  long long row_base;  // nz * rows_before[idy] * nx: the chunks of rank-grid row idy
+  int lny, off_j;      // loc_ny of row idy; j + lny * z
+};
+__device__ inline LineMap line_map(const Decomp &d, int y, int z) {
+  const int idy = y % d.py, j = y / d.py;
+  LineMap m;
+  m.lny = cyc_count(d.ny, idy, d.py);
+  m.row_base = (long long)d.nz * d.rows_before[idy] * d.nx;
+  m.off_j = j + m.lny * z;
+  return m;
+}
+__device__ inline long long chunk_pos(const Decomp &d, const LineMap &m, int x) {
   const int i = x / d.px, idx = x - i * d.px;
   const int lnx = cyc_count(d.nx, idx, d.px);
-  const long long base = (long long)d.nz * ((long long)d.rows_before[idy] * d.nx +
-                                            (long long)lny * d.cols_before[idx]);
-  return base + i + (long long)lnx * (j + (long long)lny * z);
+  return m.row_base + (long long)d.nz * m.lny * d.cols_before[idx] + i +
+         (long long)lnx * m.off_j;
 }
 
+// DIR 0: pack (global -> chunks), 1: unpack (chunks -> global); VEC: 16-B global accesses
+template <int DIR, bool VEC>
 __global__ void __launch_bounds__(kPackThreads)
-pack_columns_kernel(const float *__restrict__ global, Decomp d, float *__restrict__ send) {
-  const int x = blockIdx.x * kPackThreads + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
-  if (x >= d.nx) return;
-  send[line_pos(d, x, y, z)] = global[((long long)z * d.ny + y) * d.nx + x];
-}
-
-__global__ void __launch_bounds__(kPackThreads)
-unpack_columns_kernel(const float *__restrict__ recv, Decomp d, float *__restrict__ global) {
-  const int x = blockIdx.x * kPackThreads + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
-  if (x >= d.nx) return;
-  global[((long long)z * d.ny + y) * d.nx + x] = recv[line_pos(d, x, y, z)];
+transpose_columns_kernel(const float *__restrict__ src, long long sstride, Decomp d,
+                         float *__restrict__ dst, long long dstride, long long nlines) {
+  const long long line = (long long)blockIdx.x * kPackLines + (threadIdx.x >> 6);
+  if (line >= nlines) return;
+  const int lane = threadIdx.x & 63;
+  const int y = (int)(line % d.ny), z = (int)(line / d.ny);
+  const LineMap m = line_map(d, y, z);
+  const float *__restrict__ s = src + (long long)blockIdx.y * sstride;
+  float *__restrict__ t = dst + (long long)blockIdx.y * dstride;
+  const long long gline = line * d.nx;  // global offset of the line
+  for (int x0 = 4 * lane; x0 < d.nx; x0 += 256) {
+    if (VEC && x0 + 3 < d.nx) {
+      if (DIR == 0) {
+        const float4 v = *reinterpret_cast<const float4 *>(s + gline + x0);
+        t[chunk_pos(d, m, x0)] = v.x;
+        t[chunk_pos(d, m, x0 + 1)] = v.y;
+        t[chunk_pos(d, m, x0 + 2)] = v.z;
+        t[chunk_pos(d, m, x0 + 3)] = v.w;
+      } else {
+        float4 v;
+        v.x = s[chunk_pos(d, m, x0)];
+        v.y = s[chunk_pos(d, m, x0 + 1)];
+        v.z = s[chunk_pos(d, m, x0 + 2)];
+        v.w = s[chunk_pos(d, m, x0 + 3)];
+        *reinterpret_cast<float4 *>(t + gline + x0) = v;
+      }
+    } else {
+      const int n = min(4, d.nx - x0);
+      for (int e = 0; e < n; ++e) {
+        if (DIR == 0) t[chunk_pos(d, m, x0 + e)] = s[gline + x0 + e];
+        else t[gline + x0 + e] = s[chunk_pos(d, m, x0 + e)];
+      }
+    }
+  }
 }
 
 // tmp3d = sgemv('n', n2d*nz_ph, k, 1.0/(g*k), ph, ., x = 1, 0.0) in the reference BLAS
@@ -122,24 +159,40 @@ static dim3 grid_for(long long n) {
   return dim3((unsigned)std::min<long long>(std::max<long long>(b, 1), 1 << 20));
 }
 
+// nm member fields: member i at src + i * sstride, dst + i * dstride (elements)
+hipError_t launch_transpose_columns(hipStream_t s, bool unpack, const float *src,
+                                    long long sstride, int nm, const Decomp &d, float *dst,
+                                    long long dstride) {
+  const long long nlines = (long long)d.ny * d.nz;
+  if (nlines == 0 || d.nx == 0 || nm <= 0) return hipSuccess;
+  if (nm > 65535) return hipErrorInvalidValue;
+  const long long nb = (nlines + kPackLines - 1) / kPackLines;
+  if (nb >= (1LL << 31)) return hipErrorInvalidValue;
+  // the global side is 16-B aligned line by line when nx % 4 == 0, its base is 16-B aligned
+  // and so is every member's (stride % 4 == 0)
+  const float *g = unpack ? dst : src;
+  const long long gs = unpack ? dstride : sstride;
+  const bool vec = d.nx % 4 == 0 && (reinterpret_cast<uintptr_t>(g) & 15) == 0 &&
+                   (nm == 1 || gs % 4 == 0);
+  const dim3 grid((unsigned)nb, (unsigned)nm);
+  if (!unpack) {
+    if (vec) hipLaunchKernelGGL((transpose_columns_kernel<0, true>), grid, dim3(kPackThreads), 0, s, src, sstride, d, dst, dstride, nlines);
+    else hipLaunchKernelGGL((transpose_columns_kernel<0, false>), grid, dim3(kPackThreads), 0, s, src, sstride, d, dst, dstride, nlines);
+  } else {
+    if (vec) hipLaunchKernelGGL((transpose_columns_kernel<1, true>), grid, dim3(kPackThreads), 0, s, src, sstride, d, dst, dstride, nlines);
+    else hipLaunchKernelGGL((transpose_columns_kernel<1, false>), grid, dim3(kPackThreads), 0, s, src, sstride, d, dst, dstride, nlines);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_pack_columns(hipStream_t s, const float *global, const Decomp &d,
                                float *send) {
-  const long long n = (long long)d.nx * d.ny * d.nz;
-  if (n == 0) return hipSuccess;
-  if (d.ny > 65535 || d.nz > 65535) return hipErrorInvalidValue;
-  const dim3 grid((d.nx + kPackThreads - 1) / kPackThreads, d.ny, d.nz);
-  hipLaunchKernelGGL(pack_columns_kernel, grid, dim3(kPackThreads), 0, s, global, d, send);
-  return hipGetLastError();
+  return launch_transpose_columns(s, false, global, 0, 1, d, send, 0);
 }
 
 hipError_t launch_unpack_columns(hipStream_t s, const float *recv, const Decomp &d,
                                  float *global) {
-  const long long n = (long long)d.nx * d.ny * d.nz;
-  if (n == 0) return hipSuccess;
-  if (d.ny > 65535 || d.nz > 65535) return hipErrorInvalidValue;
-  const dim3 grid((d.nx + kPackThreads - 1) / kPackThreads, d.ny, d.nz);
-  hipLaunchKernelGGL(unpack_columns_kernel, grid, dim3(kPackThreads), 0, s, recv, d, global);
-  return hipGetLastError();
+  return launch_transpose_columns(s, true, recv, 0, 1, d, global, 0);
 }
 
 hipError_t launch_vcoord_mean(hipStream_t s, const float *ph, long long n2d, int nz_ph, int k,

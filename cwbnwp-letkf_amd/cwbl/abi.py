@@ -98,8 +98,8 @@ class KernelTime(C.Structure):
 
 #: exported symbols of the product library (include/cwb_letkf_core.h)
 EXPORTS = ["cwbl_init", "cwbl_set_stream", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch", "cwbl_search",
-           "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
-           "cwbl_member_sum", "cwbl_scale", "cwbl_set_kernel_timing", "cwbl_kernel_times",
+           "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_pack_members",
+           "cwbl_unpack_members", "cwbl_vcoord_mean", "cwbl_member_sum", "cwbl_scale", "cwbl_set_kernel_timing", "cwbl_kernel_times",
            "cwbl_set_option", "cwbl_finalize", "cwbl_last_error", "cwbl_abi_version"]
 
 
@@ -271,6 +271,8 @@ def load_library(path=None):
                                 vp, vp, C.c_int]
     lib.cwbl_pack_columns.argtypes = [vp] + [C.c_int] * 5 + [vp]
     lib.cwbl_unpack_columns.argtypes = [vp] + [C.c_int] * 5 + [vp]
+    lib.cwbl_pack_members.argtypes = [vp, C.c_longlong] + [C.c_int] * 6 + [vp, C.c_longlong]
+    lib.cwbl_unpack_members.argtypes = [vp, C.c_longlong] + [C.c_int] * 6 + [vp, C.c_longlong]
     lib.cwbl_vcoord_mean.argtypes = [vp, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_float, vp]
     lib.cwbl_member_sum.argtypes = [vp, C.c_longlong, C.c_int, vp]
     lib.cwbl_scale.argtypes = [vp, C.c_longlong, C.c_float]
@@ -281,7 +283,8 @@ def load_library(path=None):
     lib.cwbl_last_error.restype = cp
     lib.cwbl_abi_version.restype = C.c_int
     for fn in ("cwbl_init", "cwbl_set_stream", "cwbl_set_obs", "cwbl_analyze_var", "cwbl_solve_batch",
-               "cwbl_search", "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_vcoord_mean",
+               "cwbl_search", "cwbl_pack_columns", "cwbl_unpack_columns", "cwbl_pack_members",
+               "cwbl_unpack_members", "cwbl_vcoord_mean",
                "cwbl_member_sum", "cwbl_scale", "cwbl_set_kernel_timing", "cwbl_kernel_times",
                "cwbl_set_option", "cwbl_finalize"):
         getattr(lib, fn).restype = C.c_int
@@ -366,6 +369,16 @@ class Core:
         """letkf_gather_grid's receive-side unpacking (module_mpi_util.f90:326-350)."""
         self._check(self.lib.cwbl_unpack_columns(_ptr(recv), nx, ny, nz, px, py,
                                                  _ptr(global_field)))
+
+    def pack_members(self, global_fields, gstride, nm, nx, ny, nz, px, py, send, sstride):
+        """pack_columns for nm member fields in one launch (strides in elements)."""
+        self._check(self.lib.cwbl_pack_members(_ptr(global_fields), gstride, nm, nx, ny, nz,
+                                               px, py, _ptr(send), sstride))
+
+    def unpack_members(self, recv, rstride, nm, nx, ny, nz, px, py, global_fields, gstride):
+        """unpack_columns for nm member fields in one launch (strides in elements)."""
+        self._check(self.lib.cwbl_unpack_members(_ptr(recv), rstride, nm, nx, ny, nz, px, py,
+                                                 _ptr(global_fields), gstride))
 
     def vcoord_mean(self, ph, n2d, nz_ph, k, stagger, g, alt):
         """letkf_scatter_vcoord's member mean of PH/g + destagger (:491-505)."""

@@ -217,57 +217,132 @@ class Transposer:
     def _scale(self, x, n, alpha):
         self.core.scale(x, n, alpha)
 
+    # ---- member fields as one stacked tensor ----------------------------------------------------
+    @staticmethod
+    def _stacked(tensors, shape):
+        """(first tensor, stride in elements) when `tensors` are contiguous fields of `shape`
+        laid out at one constant stride (views of a stacked tensor: one launch packs them
+        all), else None."""
+        if not tensors or any(not t.is_contiguous() or tuple(t.shape) != tuple(shape)
+                              for t in tensors):
+            return None
+        n = int(np.prod(shape))
+        if len(tensors) == 1:
+            return tensors[0], n
+        base = tensors[0].untyped_storage().data_ptr()
+        if any(t.untyped_storage().data_ptr() != base for t in tensors):
+            return None
+        d = tensors[1].data_ptr() - tensors[0].data_ptr()
+        if d % 4 or d // 4 < n:
+            return None
+        if any(tensors[i].data_ptr() - tensors[0].data_ptr() != i * d for i in range(len(tensors))):
+            return None
+        return tensors[0], d // 4
+
+    def _pack(self, fields, gx, gy, nz, dst, dstride):
+        """pack_columns of every field in `fields` (a list) into dst + i * dstride: one launch
+        when the fields are a stacked tensor, else one per field."""
+        st = self._stacked(fields, (nz, gy, gx))
+        px, py = self.dec.px, self.dec.py
+        if st is not None:
+            self.core.pack_members(st[0], st[1], len(fields), gx, gy, nz, px, py, dst, dstride)
+        else:
+            for i, f in enumerate(fields):
+                assert f.is_contiguous() and tuple(f.shape) == (nz, gy, gx), tuple(f.shape)
+                n = gx * gy * nz
+                self.core.pack_columns(f, gx, gy, nz, px, py, dst.view(-1)[i * dstride:i * dstride + n])
+
+    def _unpack(self, src, sstride, outs, gx, gy, nz):
+        st = self._stacked(outs, (nz, gy, gx))
+        px, py = self.dec.px, self.dec.py
+        if st is not None:
+            self.core.unpack_members(src, sstride, len(outs), gx, gy, nz, px, py, st[0], st[1])
+        else:
+            n = gx * gy * nz
+            for i, g in enumerate(outs):
+                self.core.unpack_columns(src.reshape(-1)[i * sstride:i * sstride + n], gx, gy, nz,
+                                         px, py, g)
+
     # ---- letkf_scatter_grid (:190-262) ---------------------------------------------------------
     def scatter_grid(self, fields, nz, stagger=0, out=None):
         """fields: {m: (nz, ny', nx') device tensor} for the members this rank owns.
-        Returns var (k, nz, loc_ny, loc_nx) with every member's columns of this rank."""
+        Returns var (k, nz, loc_ny, loc_nx) with every member's columns of this rank.
+
+        On one rank the column layout IS the member layout (px = py = 1): when the fields are
+        the k views of one stacked (k, nz, ny', nx') tensor and no `out` is given, that tensor
+        is returned as var (no copy; the analysis then updates the member fields in place, as
+        gather_grid would).  Otherwise every owned member is packed in one launch."""
         torch = self.torch
         gx, gy = self.dec.grid(stagger)
         lx, ly = self.local_shape(stagger)
+        mine = self.owned()
+        n = gx * gy * nz
+        if self.world == 1 and out is None:
+            st = self._stacked([fields[m] for m in mine], (nz, gy, gx))
+            if st is not None and st[1] == n:
+                base = st[0]
+                return torch.as_strided(base, (self.k, nz, ly, lx), (n, ly * lx, lx, 1))
         var = out if out is not None else torch.empty((self.k, nz, ly, lx), dtype=torch.float32,
                                                        device=self.device)
         chunks = self.dec.chunks(nz, stagger)
         self._sync()
-        sends, recvs, keep = [], [], []
+        if self.world == 1:  # the one chunk is this rank's slab: pack straight into it
+            self._pack([fields[m] for m in mine], gx, gy, nz, var, lx * ly * nz)
+            self._sync()
+            return var
+        packed = torch.empty((max(len(mine), 1), n), dtype=torch.float32, device=self.device)
+        if mine:
+            self._pack([fields[m] for m in mine], gx, gy, nz, packed, n)
+        sends, recvs = [], []
         for m in range(self.k):
             src = self.owner(m)
             if src == self.rank:
-                f = fields[m]
-                assert f.is_contiguous() and tuple(f.shape) == (nz, gy, gx), (m, tuple(f.shape))
-                if self.world == 1:  # the one chunk is this rank's slab: pack straight into it
-                    self.core.pack_columns(f, gx, gy, nz, self.dec.px, self.dec.py, var[m].view(-1))
-                    continue
-                packed = torch.empty(gx * gy * nz, dtype=torch.float32, device=self.device)
-                self.core.pack_columns(f, gx, gy, nz, self.dec.px, self.dec.py, packed)
-                keep.append(packed)
+                i = mine.index(m)
                 for d, (off, cnt) in enumerate(chunks):
                     if d == self.rank:
-                        var[m].view(-1).copy_(packed[off:off + cnt])
+                        var[m].view(-1).copy_(packed[i, off:off + cnt])
                     elif cnt:
-                        sends.append((d, m, packed[off:off + cnt]))
+                        sends.append((d, m, packed[i, off:off + cnt]))
             elif lx * ly * nz:
                 recvs.append((src, m, var[m].view(-1)))
+        self._sync()
         self._exchange(sends, recvs)
         self._sync()
         return var
 
     # ---- letkf_gather_grid (:264-358) ------------------------------------------------------------
     def gather_grid(self, var, stagger=0, out=None):
-        """var (k, nz, loc_ny, loc_nx) -> {m: (nz, ny', nx')} for the members this rank owns."""
+        """var (k, nz, loc_ny, loc_nx) -> {m: (nz, ny', nx')} for the members this rank owns.
+        On one rank with no `out`, the result is views of var (no copy); a member field of
+        `out` that already is var's member (scatter_grid's aliasing) is left as it is."""
         torch = self.torch
         k, nz = var.shape[:2]
         gx, gy = self.dec.grid(stagger)
+        n = gx * gy * nz
         chunks = self.dec.chunks(nz, stagger)
+        mine = self.owned()
         out = out if out is not None else {}
+        if self.world == 1:
+            todo = [m for m in mine
+                    if out.get(m) is not None and out[m].data_ptr() != var[m].data_ptr()]
+            for m in mine:
+                if out.get(m) is None:
+                    out[m] = var[m].view(nz, gy, gx)
+            if todo:
+                self._sync()
+                if len(todo) == len(mine):  # all k members: var is their stack at stride n
+                    self._unpack(var, n, [out[m] for m in mine], gx, gy, nz)
+                else:
+                    for m in todo:
+                        self._unpack(var[m], n, [out[m]], gx, gy, nz)
+            return out
         self._sync()
-        sends, recvs, packed = [], [], {}
+        bufs = torch.empty((max(len(mine), 1), n), dtype=torch.float32, device=self.device)
+        sends, recvs = [], []
         for m in range(k):
             dst = self.owner(m)
-            if dst == self.rank and self.world == 1:  # unpack straight from the slab (below)
-                packed[m] = var[m].reshape(-1)
-            elif dst == self.rank:
-                buf = torch.empty(gx * gy * nz, dtype=torch.float32, device=self.device)
-                packed[m] = buf
+            if dst == self.rank:
+                buf = bufs[mine.index(m)]
                 for s, (off, cnt) in enumerate(chunks):
                     if s == self.rank:
                         buf[off:off + cnt].copy_(var[m].reshape(-1))
@@ -277,11 +352,13 @@ class Transposer:
                 sends.append((dst, m, var[m].reshape(-1).contiguous()))
         self._exchange(sends, recvs)
         self._sync()
-        for m, buf in packed.items():
-            g = out.get(m)
-            if g is None:
-                g = out[m] = torch.empty((nz, gy, gx), dtype=torch.float32, device=self.device)
-            self.core.unpack_columns(buf, gx, gy, nz, self.dec.px, self.dec.py, g)
+        missing = [m for m in mine if out.get(m) is None]
+        if missing:  # one stacked tensor, so that the unpacking is one launch
+            stk = torch.empty((len(missing), nz, gy, gx), dtype=torch.float32, device=self.device)
+            for i, m in enumerate(missing):
+                out[m] = stk[i]
+        if mine:
+            self._unpack(bufs, n, [out[m] for m in mine], gx, gy, nz)
         return out
 
     # ---- root -> columns (letkf_scatter_hcoord :360-443, vcoord stagger -1 :543-575) ----------

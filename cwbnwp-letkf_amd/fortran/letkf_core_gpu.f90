@@ -74,7 +74,8 @@ module letkf_core_gpu
     end type cwbl_projection
 
     public :: cwbl_init, cwbl_set_obs, cwbl_analyze_var, cwbl_solve_batch, cwbl_search, &
-              cwbl_pack_columns, cwbl_unpack_columns, cwbl_vcoord_mean, &
+              cwbl_pack_columns, cwbl_unpack_columns, cwbl_pack_members, cwbl_unpack_members, &
+              cwbl_vcoord_mean, &
               cwbl_member_sum, cwbl_scale, cwbl_set_stream, cwbl_set_option, &
               cwbl_finalize, cwbl_abi_version, cwbl_error, cwbl_check
     ! host obs ingest (include/cwb_letkf_ingest.h); file names and varname are passed as
@@ -131,6 +132,22 @@ module letkf_core_gpu
             type(c_ptr),    value :: recv, global
             integer(c_int), value :: nx, ny, nz, px, py
         end function cwbl_unpack_columns
+
+        integer(c_int) function cwbl_pack_members(global, gstride, nm, nx, ny, nz, px, py, &
+                send, sstride) bind(C, name='cwbl_pack_members')
+            import :: c_int, c_long_long, c_ptr
+            type(c_ptr),          value :: global, send
+            integer(c_long_long), value :: gstride, sstride
+            integer(c_int),       value :: nm, nx, ny, nz, px, py
+        end function cwbl_pack_members
+
+        integer(c_int) function cwbl_unpack_members(recv, rstride, nm, nx, ny, nz, px, py, &
+                global, gstride) bind(C, name='cwbl_unpack_members')
+            import :: c_int, c_long_long, c_ptr
+            type(c_ptr),          value :: recv, global
+            integer(c_long_long), value :: rstride, gstride
+            integer(c_int),       value :: nm, nx, ny, nz, px, py
+        end function cwbl_unpack_members
 
         integer(c_int) function cwbl_vcoord_mean(ph, n2d, nz_ph, k, stagger, g, alt) &
                 bind(C, name='cwbl_vcoord_mean')

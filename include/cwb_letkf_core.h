@@ -240,6 +240,13 @@ int         cwbl_pack_columns(const float *global, int nx, int ny, int nz, int p
 /* letkf_gather_grid's receive side (:326-350): the inverse of cwbl_pack_columns. */
 int         cwbl_unpack_columns(const float *recv, int nx, int ny, int nz, int px, int py,
                                 float *global);
+/* The same for nm member fields in one launch (the members a rank owns, k/N of them on an
+ * N-GPU node): member i is global + i*gstride -> send + i*sstride (strides in elements, >= the
+ * field's nx*ny*nz when nm > 1), and back. */
+int         cwbl_pack_members(const float *global, long long gstride, int nm, int nx, int ny,
+                              int nz, int px, int py, float *send, long long sstride);
+int         cwbl_unpack_members(const float *recv, long long rstride, int nm, int nx, int ny,
+                                int nz, int px, int py, float *global, long long gstride);
 /* letkf_scatter_vcoord's reduction (:491-505): ph(n2d, nz_ph, 0:k-1), member slowest ->
  * alt(n2d, nz_out).  tmp = sgemv('n', n2d*nz_ph, k, 1.0/(g*k), ph, ., ones, 0.0) evaluated
  * in the reference BLAS order (y = 0; y += (alpha*1)*ph(:,m), m = 0..k-1, fp32); then

@@ -48,6 +48,33 @@ def test_pack_unpack_vs_oracle(nz, ny, nx, world):
     assert torch.equal(back, f)
 
 
+@pytest.mark.parametrize("nz,ny,nx,world,nm,pad", [(3, 7, 12, 6, 5, 0), (5, 11, 9, 8, 3, 7),
+                                                     (4, 33, 64, 12, 8, 4), (50, 30, 301, 8, 5, 1),
+                                                     (50, 300, 300, 1, 4, 0), (1, 70000, 3, 2, 2, 0)])
+def test_pack_unpack_members_vs_oracle(nz, ny, nx, world, nm, pad):
+    """cwbl_pack_members / cwbl_unpack_members: nm member fields in one launch at a member
+    stride of n + pad elements (16-B global accesses where nx % 4 == 0 and every member is
+    aligned, 4-B otherwise), the rows of a line folded into the grid (ny or nz past 65535),
+    against the oracle member by member; lanes never write past a member's n elements."""
+    c = core()
+    px, py = tr.dims_create(world)
+    n = nz * ny * nx
+    st = n + pad
+    f = torch.randn((nm * st,), device="cuda", dtype=torch.float32)
+    send = torch.full((nm * st,), float("nan"), device="cuda")
+    c.pack_members(f, st, nm, nx, ny, nz, px, py, send, st)
+    got = send.cpu().numpy().reshape(nm, st)
+    fh = f.cpu().numpy().reshape(nm, st)
+    for i in range(nm):
+        np.testing.assert_array_equal(got[i, :n], mo.pack_columns(fh[i, :n].reshape(nz, ny, nx), px, py))
+        assert np.isnan(got[i, n:]).all()
+    back = torch.full_like(f, float("nan"))
+    c.unpack_members(send, st, nm, nx, ny, nz, px, py, back, st)
+    b = back.cpu().numpy().reshape(nm, st)
+    np.testing.assert_array_equal(b[:, :n], fh[:, :n])
+    assert np.isnan(b[:, n:]).all()
+
+
 @pytest.mark.parametrize("side_stream", [False, True])
 def test_device_inputs_only_need_to_be_queued(side_stream):
     """The library's streams are non-blocking; every device-pointer entry point must wait for
@@ -98,7 +125,8 @@ def test_vcoord_mean_vs_oracle(k, stagger):
 
 
 def test_transposer_local_world1():
-    """world 1: every transfer is a self copy; the packing kernels do all the work."""
+    """world 1: separate member tensors go through the packing kernels (one launch), a stacked
+    member tensor is var itself (no copy)."""
     c = core(5)
     t = tr.Transposer(c, 5, 7, 6)
     nz = 4
@@ -108,6 +136,9 @@ def test_transposer_local_world1():
     back = t.gather_grid(var)
     for m in range(5):
         assert torch.equal(back[m], members[m])
+    stk = torch.stack(members)
+    var = t.scatter_grid({m: stk[m] for m in range(5)}, nz)
+    assert var.data_ptr() == stk.data_ptr()
 
 
 def _free_port():

@@ -72,6 +72,20 @@ class OracleCore:
     def unpack_columns(self, recv, nx, ny, nz, px, py, g):
         g.copy_(torch.from_numpy(mo.unpack_columns(recv.numpy(), nz, ny, nx, px, py)))
 
+    def pack_members(self, g, gstride, nm, nx, ny, nz, px, py, send, sstride):
+        n = nx * ny * nz
+        src = torch.as_strided(g, (nm, n), (gstride, 1))
+        dst = torch.as_strided(send, (nm, n), (sstride, 1))
+        for i in range(nm):
+            dst[i].copy_(torch.from_numpy(mo.pack_columns(src[i].numpy().reshape(nz, ny, nx), px, py)))
+
+    def unpack_members(self, recv, rstride, nm, nx, ny, nz, px, py, g, gstride):
+        n = nx * ny * nz
+        src = torch.as_strided(recv, (nm, n), (rstride, 1))
+        dst = torch.as_strided(g, (nm, n), (gstride, 1))
+        for i in range(nm):
+            dst[i].copy_(torch.from_numpy(mo.unpack_columns(src[i].numpy(), nz, ny, nx, px, py).ravel()))
+
     def vcoord_mean(self, ph, n2d, nz_ph, k, stagger, gconst, alt):
         alt.copy_(torch.from_numpy(mo.vcoord_mean(ph.numpy(), stagger, np.float32(gconst))))
 
@@ -104,7 +118,11 @@ def run_plan(t, k, nx, ny, nz, out_dir, rank):
     for st in (0, 1, 2):
         gx, gy = t.dec.grid(st)
         members = fields_for(k, nz, gy, gx, 10 + st)
-        own = {m: torch.from_numpy(members[m]).to(t.device) for m in t.owned()}
+        if st == 0:  # the owned members as views of one stacked tensor (one-launch packing)
+            stk = torch.from_numpy(np.stack([members[m] for m in t.owned()])).to(t.device)
+            own = {m: stk[i] for i, m in enumerate(t.owned())}
+        else:
+            own = {m: torch.from_numpy(members[m]).to(t.device) for m in t.owned()}
         var = t.scatter_grid(own, nz, st)
         res[f"var{st}"] = var.cpu().numpy()
         back = t.gather_grid(var * 2.0, st)
@@ -233,3 +251,30 @@ def test_write_mean_gloo(tmp_path, world, k):
         # and the reference's definition up to fp32 rounding
         ref = np.mean(np.stack([allf[m][i] for m in range(k)]).astype(np.float64), axis=0)
         np.testing.assert_allclose(g, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_one_rank_transposes_alias_the_stacked_fields():
+    """On one rank the column layout is the member layout: scatter_grid returns the stacked
+    member tensor itself (no copy) and gather_grid's result is views of var; fields that are
+    not one stacked tensor (or an explicit `out`) go through the packing, with the same
+    values."""
+    k, nx, ny, nz = 3, 6, 5, 4
+    t = tr.Transposer(OracleCore(), k, nx, ny, device=torch.device("cpu"))
+    assert t.world == 1
+    members = fields_for(k, nz, ny, nx, 3)
+    stk = torch.from_numpy(np.stack(members))
+    own = {m: stk[m] for m in range(k)}
+    var = t.scatter_grid(own, nz)
+    assert var.data_ptr() == stk.data_ptr() and tuple(var.shape) == (k, nz, ny, nx)
+    back = t.gather_grid(var, out=own)
+    assert all(back[m].data_ptr() == stk[m].data_ptr() for m in range(k))
+    sep = {m: torch.from_numpy(members[m].copy()) for m in range(k)}
+    var2 = t.scatter_grid(sep, nz)
+    assert var2.data_ptr() not in [f.data_ptr() for f in sep.values()]
+    np.testing.assert_array_equal(var2.numpy(), np.stack(members))
+    out = {m: torch.zeros((nz, ny, nx)) for m in range(k)}
+    t.gather_grid(var2 * 3.0, out=out)
+    for m in range(k):
+        np.testing.assert_array_equal(out[m].numpy(), members[m] * 3.0)
+    views = t.gather_grid(var2)
+    assert views[1].data_ptr() == var2[1].data_ptr()
