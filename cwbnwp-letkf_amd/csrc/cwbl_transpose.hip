@@ -68,8 +68,11 @@ __device__ inline long long chunk_pos(const Decomp &d, const LineMap &m, int x) 
          (long long)lnx * m.off_j;
 }
 
-// DIR 0: pack (global -> chunks), 1: unpack (chunks -> global); VEC: 16-B global accesses
-template <int DIR, bool VEC>
+// DIR 0: pack (global -> chunks), 1: unpack (chunks -> global); VEC: 16-B global accesses;
+// PXV: the chunk side of a lane's four x as one float4 (px = 1: x0..x0+3 are consecutive in
+// one chunk), two float2 (px = 2: x0, x0+2 and x0+1, x0+3 pair up in the two chunks) or four
+// floats (px >= 3: each store instruction of a wave writes 64 consecutive floats of one chunk)
+template <int DIR, bool VEC, int PXV>
 __global__ void __launch_bounds__(kPackThreads)
 transpose_columns_kernel(const float *__restrict__ src, long long sstride, Decomp d,
                          float *__restrict__ dst, long long dstride, long long nlines) {
@@ -83,19 +86,34 @@ transpose_columns_kernel(const float *__restrict__ src, long long sstride, Decom
   const long long gline = line * d.nx;  // global offset of the line
   for (int x0 = 4 * lane; x0 < d.nx; x0 += 256) {
     if (VEC && x0 + 3 < d.nx) {
-      if (DIR == 0) {
-        const float4 v = *reinterpret_cast<const float4 *>(s + gline + x0);
-        t[chunk_pos(d, m, x0)] = v.x;
-        t[chunk_pos(d, m, x0 + 1)] = v.y;
-        t[chunk_pos(d, m, x0 + 2)] = v.z;
-        t[chunk_pos(d, m, x0 + 3)] = v.w;
-      } else {
-        float4 v;
-        v.x = s[chunk_pos(d, m, x0)];
-        v.y = s[chunk_pos(d, m, x0 + 1)];
-        v.z = s[chunk_pos(d, m, x0 + 2)];
-        v.w = s[chunk_pos(d, m, x0 + 3)];
+      float4 v;
+      if (DIR == 1) {
+        if constexpr (PXV == 1) {
+          v = *reinterpret_cast<const float4 *>(s + chunk_pos(d, m, x0));
+        } else if constexpr (PXV == 2) {
+          const float2 a = *reinterpret_cast<const float2 *>(s + chunk_pos(d, m, x0));
+          const float2 b = *reinterpret_cast<const float2 *>(s + chunk_pos(d, m, x0 + 1));
+          v = make_float4(a.x, b.x, a.y, b.y);
+        } else {
+          v.x = s[chunk_pos(d, m, x0)];
+          v.y = s[chunk_pos(d, m, x0 + 1)];
+          v.z = s[chunk_pos(d, m, x0 + 2)];
+          v.w = s[chunk_pos(d, m, x0 + 3)];
+        }
         *reinterpret_cast<float4 *>(t + gline + x0) = v;
+      } else {
+        v = *reinterpret_cast<const float4 *>(s + gline + x0);
+        if constexpr (PXV == 1) {
+          *reinterpret_cast<float4 *>(t + chunk_pos(d, m, x0)) = v;
+        } else if constexpr (PXV == 2) {
+          *reinterpret_cast<float2 *>(t + chunk_pos(d, m, x0)) = make_float2(v.x, v.z);
+          *reinterpret_cast<float2 *>(t + chunk_pos(d, m, x0 + 1)) = make_float2(v.y, v.w);
+        } else {
+          t[chunk_pos(d, m, x0)] = v.x;
+          t[chunk_pos(d, m, x0 + 1)] = v.y;
+          t[chunk_pos(d, m, x0 + 2)] = v.z;
+          t[chunk_pos(d, m, x0 + 3)] = v.w;
+        }
       }
     } else {
       const int n = min(4, d.nx - x0);
@@ -174,14 +192,30 @@ hipError_t launch_transpose_columns(hipStream_t s, bool unpack, const float *src
   const long long gs = unpack ? dstride : sstride;
   const bool vec = d.nx % 4 == 0 && (reinterpret_cast<uintptr_t>(g) & 15) == 0 &&
                    (nm == 1 || gs % 4 == 0);
+  // the chunk side as float4 / float2: px = 1 or 2 and every chunk offset a multiple of 4
+  // (nx % 4 == 0 makes every chunk's extents and line offsets multiples of 4 / 2 alike) and
+  // every member of the chunk buffer aligned
+  const float *ck = unpack ? src : dst;
+  const long long cs = unpack ? sstride : dstride;
+  const bool cal = vec && (reinterpret_cast<uintptr_t>(ck) & 15) == 0 && (nm == 1 || cs % 4 == 0);
+  const int pxv = cal && d.px == 1 ? 1 : cal && d.px == 2 ? 2 : 0;
   const dim3 grid((unsigned)nb, (unsigned)nm);
-  if (!unpack) {
-    if (vec) hipLaunchKernelGGL((transpose_columns_kernel<0, true>), grid, dim3(kPackThreads), 0, s, src, sstride, d, dst, dstride, nlines);
-    else hipLaunchKernelGGL((transpose_columns_kernel<0, false>), grid, dim3(kPackThreads), 0, s, src, sstride, d, dst, dstride, nlines);
+#define CWBL_TRANSPOSE_LAUNCH(DIR, VEC, PXV)                                                   \
+  hipLaunchKernelGGL((transpose_columns_kernel<DIR, VEC, PXV>), grid, dim3(kPackThreads), 0, s, \
+                     src, sstride, d, dst, dstride, nlines)
+  if (!vec) {
+    if (!unpack) CWBL_TRANSPOSE_LAUNCH(0, false, 0);
+    else CWBL_TRANSPOSE_LAUNCH(1, false, 0);
+  } else if (!unpack) {
+    if (pxv == 1) CWBL_TRANSPOSE_LAUNCH(0, true, 1);
+    else if (pxv == 2) CWBL_TRANSPOSE_LAUNCH(0, true, 2);
+    else CWBL_TRANSPOSE_LAUNCH(0, true, 0);
   } else {
-    if (vec) hipLaunchKernelGGL((transpose_columns_kernel<1, true>), grid, dim3(kPackThreads), 0, s, src, sstride, d, dst, dstride, nlines);
-    else hipLaunchKernelGGL((transpose_columns_kernel<1, false>), grid, dim3(kPackThreads), 0, s, src, sstride, d, dst, dstride, nlines);
+    if (pxv == 1) CWBL_TRANSPOSE_LAUNCH(1, true, 1);
+    else if (pxv == 2) CWBL_TRANSPOSE_LAUNCH(1, true, 2);
+    else CWBL_TRANSPOSE_LAUNCH(1, true, 0);
   }
+#undef CWBL_TRANSPOSE_LAUNCH
   return hipGetLastError();
 }
 

@@ -50,7 +50,9 @@ def test_pack_unpack_vs_oracle(nz, ny, nx, world):
 
 @pytest.mark.parametrize("nz,ny,nx,world,nm,pad", [(3, 7, 12, 6, 5, 0), (5, 11, 9, 8, 3, 7),
                                                      (4, 33, 64, 12, 8, 4), (50, 30, 301, 8, 5, 1),
-                                                     (50, 300, 300, 1, 4, 0), (1, 70000, 3, 2, 2, 0)])
+                                                     (50, 300, 300, 1, 4, 0), (1, 70000, 3, 2, 2, 0),
+                                                     (10, 20, 40, 2, 3, 0), (8, 12, 16, 4, 2, 4),
+                                                     (6, 9, 20, 1, 3, 2)])
 def test_pack_unpack_members_vs_oracle(nz, ny, nx, world, nm, pad):
     """cwbl_pack_members / cwbl_unpack_members: nm member fields in one launch at a member
     stride of n + pad elements (16-B global accesses where nx % 4 == 0 and every member is
