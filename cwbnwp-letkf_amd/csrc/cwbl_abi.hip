@@ -204,7 +204,7 @@ struct TreeBufs {
 enum KernelId {
   KT_SEARCH_BINNED, KT_SEARCH_FLAGGED, KT_SEARCH_TREE, KT_ASSEMBLE_RECORD, KT_SOLVE_TQ40,
   KT_BIG_HANDOFF, KT_TQB_TAIL, KT_SOLVE_TQ, KT_SOLVE_TQ_BIG, KT_SOLVE_JACOBI, KT_TUNE_Q,
-  KT_COUNT
+  KT_BAND_HEAD, KT_BAND_TAIL, KT_COUNT
 };
 struct KTime { long long launches = 0, points = 0; double ms = 0.0; };
 
@@ -246,7 +246,8 @@ struct State {
   bool jacobi = false;                                // CWBL_SOLVER=jacobi: eigen path
   int tq4 = 1;  // CWBL_TQ4: KP=40 solve 0 = one kernel, else assembly record + solve_tq40
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: record batch (points)
-  bool big_split = true;                              // CWBL_BIG_SPLIT=0: one-kernel KP=128 solve
+  bool big_split = true;                              // big_path 1: hand-off + one-wave tail
+  bool band = false;                                  // big_path 2 (KP = 128): two-stage band path
   long long big_sub = 98304;                          // CWBL_BIG_SUB: KP=128 hand-off batch
   std::vector<hipEvent_t> events;
   hipStream_t h2d = nullptr, d2h = nullptr;           // host-memory slab copies (pipelined)
@@ -417,6 +418,8 @@ std::string kernel_name(int id) {
     case KT_SOLVE_TQ_BIG: return "solve_tq_big_kernel<" + kp + ", false>";
     case KT_SOLVE_JACOBI: return "solve_kernel<" + kp + ", false>";
     case KT_TUNE_Q: return "tune_q_kernel";
+    case KT_BAND_HEAD: return "band_head_kernel<false>";
+    case KT_BAND_TAIL: return "band_tail_kernel";
   }
   return "?";
 }
@@ -767,6 +770,7 @@ int cwbl_init(const cwbl_init_params *p) {
   // kernel's duration its own (the per-kernel timing and the roofline read it).
   S.tq40_streams = false;
   S.big_split = true;
+  S.band = false;
   // (C4 per variable, r3: 32 k points 2.42 s, 16 k 2.47, 64 k 2.41, 96 k 2.39, 128 k 2.39)
   S.big_sub = 98304;
   S.binned = true;
@@ -814,8 +818,9 @@ int cwbl_set_option(int option, long long value) {
       S.binned = value == 0;
       return CWBL_OK;
     case CWBL_OPT_BIG_PATH:
-      if (!range(0, 1)) break;
+      if (!range(0, 2)) break;
       S.big_split = value == 1;
+      S.band = value == 2;
       return CWBL_OK;
     case CWBL_OPT_BIG_BATCH:
       if (!range(64, 1LL << 24)) break;
@@ -1196,7 +1201,8 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   // busy, the four-point solve is latency-bound).  Two record and two info buffers; an
   // assembly waits for the solve two record batches back (record reuse) and for the info
   // reduction two search batches back (info reuse).
-  const bool big_split_path = (S.kp == 96 || S.kp == kBigSplitKP) && S.big_split &&
+  const bool band_path = S.kp == kBigSplitKP && S.band && S.k > 96;
+  const bool big_split_path = !band_path && (S.kp == 96 || S.kp == kBigSplitKP) && S.big_split &&
                               S.k > big_split_j0(S.kp) + 2;
   // (r4, measured and dropped: the same two-stream scheme for the k > 64 split path, the
   // tail of a hand-off sub-batch beside the next sub-batch's 256-thread kernel: +0.5%)
@@ -1271,7 +1277,29 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
       HIPCHK(hipStreamWaitEvent(S.stream, hv, 0));
     }
     HIPCHK(hipEventRecord(b2, S.stream));
-    if (big_split_path) {
+    if (band_path) {
+      // band_head_kernel (assembly + 15 panel block reflectors to a band of half-bandwidth 8)
+      // -> workspace -> band_tail_kernel (chase, quadrature, back-transform), in sub-batches of
+      // Bs points (a multiple of kListLanes) bounded by the hand-off budget
+      const size_t rec_bytes = band_record_bytes();
+      const long long fit = std::max<long long>(
+          kListLanes, (long long)(S.handoff_budget / rec_bytes) / kListLanes * kListLanes);
+      const long long cap = std::min<long long>(S.big_sub, fit);
+      const long long nsub = (nb + cap - 1) / cap;
+      long long Bs = (nb + nsub - 1) / nsub;
+      Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
+      HIPCHK(S.wsa.ensure((size_t)Bs * rec_bytes));
+      for (long long s0 = 0; s0 < nb; s0 += Bs) {
+        const int ns = (int)std::min<long long>(Bs, nb - s0);
+        HIPCHK(kt_begin(S.stream, &kt));
+        HIPCHK(launch_band_head(S.stream, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,
+                                nidx + s0 * list_cap, infob + s0, S.wsa.as<double>()));
+        HIPCHK(kt_end(S.stream, kt, KT_BAND_HEAD, ns));
+        HIPCHK(kt_begin(S.stream, &kt));
+        HIPCHK(launch_band_tail(S.stream, c, sd, g0 + s0, ns, S.wsa.as<double>(), infob + s0));
+        HIPCHK(kt_end(S.stream, kt, KT_BAND_TAIL, ns));
+      }
+    } else if (big_split_path) {
       // 256-thread assembly + first kBigJ0 steps -> workspace -> one-wavefront tail, in
       // hand-off batches of Bs points (a multiple of kListLanes; BigHandoff<128, 64> is
       // 134.7 KB per point, 13 GB at the default 98 304, outside workspace_bytes)

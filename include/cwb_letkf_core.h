@@ -300,7 +300,8 @@ enum {
   CWBL_OPT_SEARCH = 5,         /* 0 uniform bins + tree for truncated lists (default); 1 the
                                 * k-d tree walk for every point */
   CWBL_OPT_BIG_PATH = 6,       /* k = 65..128: 1 256-thread hand-off + one-wave tail (default);
-                                * 0 one 256-thread kernel */
+                                * 0 one 256-thread kernel; 2 (k = 97..128) two-stage: band
+                                * reduction on the matrix cores + one-wave bulge chase */
   CWBL_OPT_BIG_BATCH = 7,      /* points per k > 64 sub-batch (>= 64; default 98 304) */
   CWBL_OPT_PAGEABLE = 8,       /* pageable host slab: 0 page-lock in place (default); 1 bounce
                                 * through the library's page-locked slots */
