@@ -27,84 +27,9 @@
 // The design is checked step for step by scripts/two_stage_b8.py (numpy; the same panels,
 // schedule, storage bounds and application orders).  Padding rows (k < 128) are identity rows
 // of A: their panel reflectors and chase reflectors are exact no-ops (tau = 0).
-#include "cwbl_device.h"
-
-#include <type_traits>
-#include <utility>
+#include "cwbl_band.h"
 
 namespace cwbl {
-
-namespace {
-
-template <int... Is, class F>
-__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, Is...>, F &&f) {
-  (f(std::integral_constant<int, Is>{}), ...);
-}
-// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>), in order
-template <int N, class F>
-__device__ __forceinline__ void sfor(F &&f) {
-  sfor_impl(std::make_integer_sequence<int, N>{}, f);
-}
-
-// value of lane L of this lane's 16-lane row (DPP row_newbcast, one v_mov_b64)
-template <int L>
-__device__ __forceinline__ double rbcast(double x) {
-  return __longlong_as_double(
-      __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x150 + L, 0xf, 0xf, true));
-}
-// value of lane l ^ 8 of the row (row_ror:8)
-__device__ __forceinline__ double ror8(double x) { return dpp_f64<0x128>(x); }
-// sum over each 8-lane half of a 16-lane row (quad sums, then the half mirror)
-__device__ __forceinline__ double rsum8(double v) {
-  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f64<0x141>(v);  // row_half_mirror
-  return v;
-}
-
-}  // namespace
-
-// ---- the workspace record of one point ------------------------------------------------------
-struct BandRec {
-  static constexpr int N = 128, B = 8, NP = 15, NTASK = 1056;
-  static constexpr int BAND = 0;                // [N][B+1]: A(i, i-d), d = 0..B
-  static constexpr int U1 = BAND + N * (B + 1);   // Q1^T b1
-  static constexpr int U2 = U1 + N;               // Q1^T x'
-  static constexpr int PV = U2 + N;               // panel p: V (m_p x 8 row-major), m_p = 120-8p
-  static constexpr int PT = PV + 8 * 960;         // panel p: T (8 x 8, upper)
-  static constexpr int R2 = PT + NP * 64;         // chase reflector q: [q][0] tau, [q][e] v_e
-  static constexpr int WORDS = R2 + NTASK * 8;
-  __host__ __device__ static constexpr int pv(int p) { return PV + 8 * (120 * p - 4 * p * (p - 1)); }
-};
-static_assert(BandRec::pv(15) == BandRec::PT, "panel reflector offsets");
-
-// the chase schedule (scripts/two_stage_b8.py: schedule): tasks of sweep j, their first index,
-// and the round in which sweep j starts (two slots, sweep j+1 three tasks behind sweep j)
-struct ChasePlan {
-  short start[126], first[127], ntask[126];
-  int rounds;
-};
-__host__ __device__ constexpr int chase_ntask(int j) { return j <= 125 ? (125 - j) / 8 + 1 : 0; }
-__host__ __device__ constexpr ChasePlan make_chase_plan() {
-  ChasePlan p{};
-  int acc = 0, end = 0;
-  for (int j = 0; j < 126; ++j) {
-    int s = 0;
-    if (j >= 1 && p.start[j - 1] + 3 > s) s = p.start[j - 1] + 3;
-    if (j >= 2 && p.start[j - 2] + p.ntask[j - 2] > s) s = p.start[j - 2] + p.ntask[j - 2];
-    p.start[j] = (short)s;
-    p.ntask[j] = (short)chase_ntask(j);
-    p.first[j] = (short)acc;
-    acc += p.ntask[j];
-    if (s + p.ntask[j] > end) end = s + p.ntask[j];
-  }
-  p.first[126] = (short)acc;
-  p.rounds = end;
-  return p;
-}
-constexpr ChasePlan kChase = make_chase_plan();
-static_assert(kChase.first[126] == BandRec::NTASK && kChase.rounds == 586, "chase plan");
-__constant__ ChasePlan cChase = kChase;
 
 // ==== stage 1: assembly + band reduction ====================================================
 constexpr int kBandChunk = 64;
@@ -624,351 +549,6 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
   if (tid == 0) info[gi] = make_int2(ptot, 0);
 }
 
-// ==== stage 2: chase, quadrature, back-transform, epilogue ===================================
-struct BandTailSmem {
-  union {
-    double band[128][16];  // the chase: row i holds A(i, i - d), d = 0..15
-    double tq[129][4];     // then d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
-    double y[128];         // then y for the back-transform
-  } a;
-  union {
-    double u[2][128];      // Q1^T b1, Q1^T x' through the chase's reflectors
-    struct {
-      double Ym[128], Zm[128];  // quadrature sum / exact solve, walk order
-    } q;
-  } b;
-};
-
-__global__ void __launch_bounds__(64, 2)
-band_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts, double *__restrict__ ws,
-                 int2 *__restrict__ info) {
-  constexpr int KP = 128, H = KP / 2;
-  using HR = BandRec;
-  __shared__ BandTailSmem sm;
-  const int gi = xcd_remap(blockIdx.x, gridDim.x);
-  if (gi >= npts) return;
-  const int l = threadIdx.x;
-  const int k = c.k;
-  const int ptot = info[gi].x;
-  if (ptot == 0) return;  // var unchanged
-  double *__restrict__ rec = ws + (long long)gi * HR::WORDS;
-
-  long long P = 0;
-  {
-    const long long g = g0 + gi;
-    const int i = (int)(g % slab.ix_lim);
-    const long long rr = g / slab.ix_lim;
-    const int jj = (int)(rr % slab.iy_lim);
-    const int kz = (int)(rr / slab.iy_lim);
-    P = i + (long long)slab.nx * (jj + (long long)slab.ny * kz);
-  }
-  const bool mem0 = l < k, mem1 = 64 + l < k;
-  const float xb0v = slab.var[P + slab.L * (mem0 ? l : 0)];
-  const float xb1v = slab.var[P + slab.L * (mem1 ? 64 + l : 0)];
-  const float xb0 = mem0 ? xb0v : 0.0f, xb1 = mem1 ? xb1v : 0.0f;
-
-  // ---- the band into LDS --------------------------------------------------------------------
-  for (int e = l; e < 128 * 16; e += 64) {
-    const int i = e >> 4, d = e & 15;
-    sm.a.band[i][d] = d <= HR::B ? rec[HR::BAND + i * (HR::B + 1) + d] : 0.0;
-  }
-  sm.b.u[0][l] = rec[HR::U1 + l];
-  sm.b.u[0][64 + l] = rec[HR::U1 + 64 + l];
-  sm.b.u[1][l] = rec[HR::U2 + l];
-  sm.b.u[1][64 + l] = rec[HR::U2 + 64 + l];
-  __syncthreads();
-
-  // ---- the chase: rounds of up to two tasks (slot 0: even sweeps, slot 1: odd sweeps) ------
-  // lanes of a slot: row 0 = lanes 0-7 left block (and the reflector), 8-15 diagonal block;
-  // row 1 = lanes 0-7 the bulge rows below, 8-15 idle
-  const int slot = l >> 5, rr = (l >> 4) & 1, lo = l & 15;
-  const int e8 = lo & 7;
-  const bool rA = rr == 0 && lo < 8, rB = rr == 0 && lo >= 8, rC = rr == 1 && lo < 8;
-  int js = slot;  // this slot's current sweep
-  double *__restrict__ r2 = rec + HR::R2;
-  for (int R = 0; R < cChase.rounds; ++R) {
-    const int st = js <= 125 ? cChase.start[js] : 1 << 30;
-    const int t = R - st;
-    const bool act = js <= 125 && t >= 0 && t < cChase.ntask[js];
-    const int j = js <= 125 ? js : 0;
-    const int r = j + 1 + 8 * (act ? t : 0);
-    const int cc = (act && t > 0) ? r - 8 : j;  // the annihilated column
-    const int L = min(8, 128 - r);              // reflector length (>= 2 for a task)
-    // column entries x_e = A(r + e, cc) on lanes 0-7 of both rows
-    double xe = 0.0;
-    if (act && lo < 8 && e8 < L) xe = sm.a.band[r + e8][r + e8 - cc];
-    const double sq = lo < 8 && e8 >= 1 ? xe * xe : 0.0;
-    const double xx = rbcast<0>(rsum8(sq));
-    const double alpha = rbcast<0>(xe);
-    const double a2 = fma(alpha, alpha, xx);
-    const double rs = rsq64(a2);
-    const bool nz = xx > 0.0;
-    const double bt = -copysign(a2 * rs, alpha);
-    const double beta = nz ? bt : alpha;
-    const double tau = nz ? (bt - alpha) * -copysign(rs, alpha) : 0.0;
-    const double scal = nz ? rcp64(alpha - bt) : 0.0;
-    const double v = lo < 8 ? (e8 == 0 ? 1.0 : xe * scal) : 0.0;  // v_e on lanes e of a row
-    // this lane's 8-vector: A column (left block), A row (diagonal block, both triangles
-    // from the lower storage), A row (bulge rows below)
-    double X[8];
-    int rowX = 0;  // the band row of the lane's vector (A, C: varies with e; B: r + b)
-    const int b = lo - 8;
-    const int colA = cc + 1 + lo;            // role A's column
-    const bool vA = act && rA && t > 0 && lo < 7;
-    const bool vB = act && rB && b < L;
-    const int rowC = r + 8 + lo;
-    const bool vC = act && rC && L == 8 && rowC < 128;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      double x = 0.0;
-      if (e < L) {
-        if (vA) x = sm.a.band[r + e][r + e - colA];
-        else if (vB) x = e <= b ? sm.a.band[r + b][b - e] : sm.a.band[r + e][e - b];
-        else if (vC) x = sm.a.band[rowC][8 + lo - e];
-      }
-      X[e] = x;
-    }
-    (void)rowX;
-    // v^T X on every lane (v_e from lane e of the row)
-    double dot = 0.0;
-    sfor<8>([&](auto ee) {
-      constexpr int e = decltype(ee)::value;
-      dot = fma(rbcast<e>(v), X[e], dot);
-    });
-    // the diagonal block (lanes 8-15 of row 0): p = tau D v, w = p - 1/2 tau (v^T p) v
-    const double vb = ror8(v);  // v_b on lane 8 + b
-    const double s1 = rsum8(vb * dot);
-    const double wB = tau * fma(-0.5 * tau, s1 * vb, dot);
-    const double al = rB ? wB : tau * dot;
-    const double be = rB ? vb : 0.0;
-    // X -= al v + be w  (one-sided: tau (v^T X) v; two-sided: w_b v + v_b w)
-    sfor<8>([&](auto ee) {
-      constexpr int e = decltype(ee)::value;
-      X[e] = fma(-al, rbcast<e>(v), X[e]);
-      X[e] = fma(-be, rbcast<8 + e>(wB), X[e]);
-    });
-    // stores: the annihilated column, the blocks, the reflector
-    if (act && rA && lo < L) sm.a.band[r + lo][r + lo - cc] = lo == 0 ? beta : 0.0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (e < L) {
-        if (vA) sm.a.band[r + e][r + e - colA] = X[e];
-        else if (vB && e <= b) sm.a.band[r + b][b - e] = X[e];
-        else if (vC) sm.a.band[rowC][8 + lo - e] = X[e];
-      }
-    }
-    if (act && rA) r2[(cChase.first[j] + t) * 8 + lo] = lo == 0 ? tau : (lo < L ? v : 0.0);
-    if (act && t + 1 == cChase.ntask[js]) js += 2;
-    __syncthreads();
-  }
-  // ---- T: d_i = A(i, i), c(i-1, i) = A(i, i-1) ------------------------------------------------
-  double dA = sm.a.band[l][0], eA = sm.a.band[l][1];
-  double dB = sm.a.band[64 + l][0], eB = sm.a.band[64 + l][1];
-  __syncthreads();
-  sm.a.tq[l][0] = dA;
-  sm.a.tq[l][1] = l == 0 ? 0.0 : eA;
-  sm.a.tq[64 + l][0] = dB;
-  sm.a.tq[64 + l][1] = eB;
-  if (l == 0) sm.a.tq[KP][1] = 0.0;
-  // ---- Q2^T applied to u1, u2: sweep after sweep, a sweep's reflectors (disjoint rows) 8 at a
-  // time: lane = reflector tt (l >> 3) + 8 pass, entry e = l & 7
-  auto apply_sweep = [&](double *u0, double *u1v, int j, int pass, bool both) {
-    const int tt = 8 * pass + (l >> 3), e = l & 7;
-    const bool ok = tt < cChase.ntask[j];
-    const int r = j + 1 + 8 * tt;
-    const int L = min(8, 128 - r);
-    const double *q = r2 + (ok ? cChase.first[j] + tt : 0) * 8;
-    const double tu = ok ? q[0] : 0.0;
-    const double ve = ok && e < L ? (e == 0 ? 1.0 : q[e]) : 0.0;
-    const int row = ok && e < L ? r + e : 0;
-    const double a0 = ve * u0[row];
-    const double d0 = rsum8(a0);
-    double d1 = 0.0;
-    if (both) d1 = rsum8(ve * u1v[row]);
-    __syncthreads();
-    if (ok && e < L) {
-      u0[row] = fma(-tu * d0, ve, u0[row]);
-      if (both) u1v[row] = fma(-tu * d1, ve, u1v[row]);
-    }
-    __syncthreads();
-  };
-  for (int j = 0; j < 126; ++j)
-    for (int pass = 0; 8 * pass < cChase.ntask[j]; ++pass)
-      apply_sweep(sm.b.u[0], sm.b.u[1], j, pass, true);
-  sm.a.tq[l][2] = sm.b.u[0][l];
-  sm.a.tq[64 + l][2] = sm.b.u[0][64 + l];
-  sm.a.tq[l][3] = sm.b.u[1][l];
-  sm.a.tq[64 + l][3] = sm.b.u[1][64 + l];
-  __syncthreads();
-  // trace of T (= trace of A) for the spectrum bound
-  double trace = 0.0;
-  {
-    double tp = 0.0;
-    if (l < k) tp += sm.a.tq[l][0];
-    if (64 + l < k) tp += sm.a.tq[64 + l][0];
-    trace = wave_sum_dpp(tp);
-  }
-
-  // ---- T^-1/2 u2 by quadrature, u1^T T^-1 u2 exactly (the tail kernel's rule) ----------------
-  const double m = (double)c.inflat;
-  const double ratio = trace / m - (double)(k - 1);
-  int level = 1;
-  double dec = 10.0;
-  while (level < kQuadLevels && dec < ratio) {
-    dec *= 10.0;
-    ++level;
-  }
-  {
-    const int node = l & 31, side = l >> 5;
-    const int npass = quad_passes(level);
-    const double2 *rule = quad_rule(c.quad_r, npass == 1 ? 4 : 8, level);
-    for (int pass = 0; pass < npass; ++pass) {
-      const bool exact = pass == 0 && node == 31;
-      double sigma = 0.0, omega = 0.0;
-      if (!exact) {
-        const double2 tw = rule[31 * pass + node];
-        sigma = m * tw.x;
-        omega = sqrt(m) * tw.y;
-      }
-      const unsigned q0 = side ? (KP - 1) * 32u : 0u, dirb = side ? (unsigned)-32 : 32u;
-      const unsigned csb = side ? 40u : 8u;
-      auto fwd = [&](int t, double &dl, double &gt) {
-        const unsigned o = opaque_after(q0, dl) + dirb * (unsigned)t;
-        const double ct = lds_at(sm.a.tq, o + csb);
-        const double lt = ct * rcp64(dl);
-        dl = fma(-lt, ct, lds_at(sm.a.tq, o) + sigma);
-        gt = fma(-lt, gt, lds_at(sm.a.tq, o + 24));
-      };
-      constexpr int S = 8, NS = H / S;
-      double ckd[NS], ckg[NS];
-      double dl = lds_at(sm.a.tq, q0) + sigma, gt = lds_at(sm.a.tq, q0 + 24);
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        ckd[s] = dl;
-        ckg[s] = gt;
-#pragma unroll
-        for (int t = S * s + 1; t < S * s + S; ++t) fwd(t, dl, gt);
-        if (s + 1 < NS) fwd(S * s + S, dl, gt);
-      }
-      const double cm = sm.a.tq[H][1];
-      const double dlo = __shfl_xor(dl, 32, 64), go = __shfl_xor(gt, 32, 64);
-      double xv = (gt * dlo - cm * go) / fma(dl, dlo, -cm * cm);
-      double *ym = sm.b.q.Ym + side * H, *zm = sm.b.q.Zm + side * H;
-      for (int s = NS - 1; s >= 0; --s) {
-        double hh[S], mmv[S];
-        double d2 = ckd[s], g2 = ckg[s];
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-          const int t = S * s + i;
-          if (i > 0) fwd(t, d2, g2);
-          const double rd = rcp64(d2);
-          hh[i] = g2 * rd;
-          mmv[i] = (t + 1 < H)
-                       ? lds_at(sm.a.tq, opaque_after(q0, d2) + dirb * (unsigned)(t + 1) + csb) * rd
-                       : 0.0;
-        }
-#pragma unroll
-        for (int i = S - 1; i >= 0; --i) {
-          const int t = S * s + i;
-          if (t != H - 1) xv = fma(-mmv[i], xv, hh[i]);
-          const double ys = half_sum_dpp(omega * xv);
-          if (node == 0) ym[t] = pass ? ym[t] + ys : ys;
-          if (exact) zm[t] = xv;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  auto walk = [](int i) { return i < H ? i : H + (KP - 1 - i); };
-  const double d = wave_sum_dpp(fma(sm.a.tq[l][2], sm.b.q.Zm[walk(l)],
-                                    sm.a.tq[64 + l][2] * sm.b.q.Zm[walk(64 + l)]));
-  double y0 = sm.b.q.Ym[walk(l)], y1 = sm.b.q.Ym[walk(64 + l)];
-  __syncthreads();
-  // ---- y <- Q1 Q2 y: the chase's reflectors sweep by sweep in reverse, then the panels -------
-  sm.a.y[l] = y0;
-  sm.a.y[64 + l] = y1;
-  __syncthreads();
-  for (int j = 125; j >= 0; --j)
-    for (int pass = 0; 8 * pass < cChase.ntask[j]; ++pass)
-      apply_sweep(sm.a.y, nullptr, j, pass, false);
-  y0 = sm.a.y[l];
-  y1 = sm.a.y[64 + l];
-  for (int p = HR::NP - 1; p >= 0; --p) {
-    const int r0 = 8 * p + 8, mrows = 128 - r0;
-    const double *pv = rec + HR::pv(p);
-    const double *pt = rec + HR::PT + 64 * p;
-    // lane l: rows l and 64 + l (row index >= r0 only)
-    const int ia = l - r0, ib = 64 + l - r0;
-    const bool va = ia >= 0 && ia < mrows, vb = ib >= 0 && ib < mrows;
-    double Va[8], Vbb[8], s[8];
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      Va[a] = va ? pv[ia * 8 + a] : 0.0;
-      Vbb[a] = vb ? pv[ib * 8 + a] : 0.0;
-      s[a] = fma(Va[a], y0, Vbb[a] * y1);
-    }
-    wave_sum4_dpp(s[0], s[1], s[2], s[3]);
-    wave_sum4_dpp(s[4], s[5], s[6], s[7]);
-    double z[8];  // z = T s (T upper)
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      double acc = 0.0;
-#pragma unroll
-      for (int bq = a; bq < 8; ++bq) acc = fma(pt[a * 8 + bq], s[bq], acc);
-      z[a] = acc;
-    }
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      y0 = fma(-Va[a], z[a], y0);
-      y1 = fma(-Vbb[a], z[a], y1);
-    }
-  }
-
-  // ---- analysis and RTPP / RTPS (:671-698), fp32 in the reference's order --------------------
-  auto seq_sum_f32 = [&](float a0, float a1) {
-    float s = 0.0f;
-    for (int mm = 0; mm < 64; ++mm) s = s + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a0), mm));
-    for (int mm = 64; mm < k; ++mm) s = s + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a1), mm - 64));
-    return s;
-  };
-  const double xb_mean = (double)(seq_sum_f32(xb0, xb1) * c.nmember_inv);  // fp32 (:671)
-  const double sk = sqrt((double)(k - 1));
-  float xa0 = mem0 ? (float)(xb_mean + (d + sk * y0)) : 0.0f;
-  float xa1 = mem1 ? (float)(xb_mean + (d + sk * y1)) : 0.0f;
-  if (c.use_rtpp || c.use_rtps) {
-    const float xa_mean = seq_sum_f32(xa0, xa1) * c.nmember_inv;
-    const double xp0 = mem0 ? (double)xb0 - xb_mean : 0.0;
-    const double xp1 = mem1 ? (double)xb1 - xb_mean : 0.0;
-    float xap0 = mem0 ? xa0 - xa_mean : 0.0f;
-    float xap1 = mem1 ? xa1 - xa_mean : 0.0f;
-    if (c.use_rtpp) {
-      if (mem0) xap0 = (float)((double)((1.0f - c.rtpp_alpha) * xap0) + (double)c.rtpp_alpha * xp0);
-      if (mem1) xap1 = (float)((double)((1.0f - c.rtpp_alpha) * xap1) + (double)c.rtpp_alpha * xp1);
-    }
-    if (c.use_rtps) {
-      double d8 = 0.0;
-      for (int mm = 0; mm < 64; ++mm) {
-        const double xp = readlane_f64(xp0, mm);
-        d8 = d8 + xp * xp;
-      }
-      for (int mm = 64; mm < k; ++mm) {
-        const double xp = readlane_f64(xp1, mm - 64);
-        d8 = d8 + xp * xp;
-      }
-      const float xb_std = (float)d8;
-      const float xa_std = seq_sum_f32(xap0 * xap0, xap1 * xap1);
-      const float f = c.rtps_alpha * sqrtf(xb_std / xa_std) - c.rtps_alpha + 1.0f;
-      xap0 = xap0 * f;
-      xap1 = xap1 * f;
-    }
-    xa0 = xa_mean + xap0;
-    xa1 = xa_mean + xap1;
-  }
-  if (mem0) slab.var[P + slab.L * l] = xa0;
-  if (mem1) slab.var[P + slab.L * (64 + l)] = xa1;
-  if (l == 0) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
-}
-
 hipError_t launch_band_head(hipStream_t s, const TreeDesc *trees, SolveConsts c, SlabDev slab,
                             long long g0, int npts, const int *nbr_cnt, const int *nbr_idx,
                             int2 *info, double *ws) {
@@ -976,14 +556,6 @@ hipError_t launch_band_head(hipStream_t s, const TreeDesc *trees, SolveConsts c,
   if (c.kp != 128 || c.k <= 96) return hipErrorInvalidValue;
   hipLaunchKernelGGL((band_head_kernel<false>), dim3(npts), dim3(256), 0, s, trees, c, slab, g0,
                      npts, nbr_cnt, nbr_idx, info, ws);
-  return hipGetLastError();
-}
-
-hipError_t launch_band_tail(hipStream_t s, SolveConsts c, SlabDev slab, long long g0, int npts,
-                            double *ws, int2 *info) {
-  if (npts <= 0) return hipSuccess;
-  if (c.quad == nullptr || c.kp != 128 || c.k <= 96) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(band_tail_kernel, dim3(npts), dim3(64), 0, s, c, slab, g0, npts, ws, info);
   return hipGetLastError();
 }
 
