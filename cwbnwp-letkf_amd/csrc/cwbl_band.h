@@ -43,6 +43,22 @@ __device__ __forceinline__ double fnmac_row(double acc, double x, double y) {
   return acc;
 }
 __device__ __forceinline__ void dpp_pin(double &x) { asm volatile("s_nop 1" : "+v"(x)); }
+// the same as volatile statements: kept in program order relative to each other and to the
+// volatile s_nop that opens a pass (dpp_fence), so no VALU write of a DPP source lands within
+// two instructions of its read
+template <int L>
+__device__ __forceinline__ double fmac_row_v(double acc, double x, double y) {
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+               : "+v"(acc) : "v"(x), "v"(y), "i"(L));
+  return acc;
+}
+template <int L>
+__device__ __forceinline__ double fnmac_row_v(double acc, double x, double y) {
+  asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+               : "+v"(acc) : "v"(x), "v"(y), "i"(L));
+  return acc;
+}
+__device__ __forceinline__ void dpp_fence() { asm volatile("s_nop 1" ::: "memory"); }
 // value of lane l ^ 8 of the row (row_ror:8)
 __device__ __forceinline__ double ror8(double x) { return dpp_f64<0x128>(x); }
 // sum over each 8-lane half of a 16-lane row (quad sums, then the half mirror)

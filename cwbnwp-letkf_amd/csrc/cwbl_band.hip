@@ -218,9 +218,22 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
     // (no barrier here: T, Z and M of the previous panel were last read before its barrier B3,
     // and a wave reaches this panel's B1 only after its part of the previous update)
     if (wave == owner) {
-      // -- the panel QR, in place in tile column Q (slot SL), columns 8H .. 8H + 7 --------------
-      auto qr = [&](auto SL_, auto H_) {
-        constexpr int SL = decltype(SL_)::value, H = decltype(H_)::value;
+      // -- the panel QR, in place in tile column Q, columns 8H .. 8H + 7 -----------------------
+      // The QR runs on slot 0's registers: a wave whose panel lies in its second tile column
+      // swaps its two slots around it (the tile order of the rest is per slot, so only the QR
+      // needs to know).
+      const bool swp = Q != I0;
+      auto swap_slots = [&]() {
+        sfor<8>([&](auto JJ) {
+          constexpr int J = decltype(JJ)::value;
+          const f64x4 t0 = tile[J];
+          tile[J] = tile[8 + J];
+          tile[8 + J] = t0;
+        });
+      };
+      if (swp) swap_slots();
+      auto qr = [&](auto H_) {
+        constexpr int H = decltype(H_)::value;
         constexpr int C0 = 8 * H;
         // band: the diagonal block D_p (rows 8p + a, columns 8p + b, b <= a): tile (Q, Q),
         // rows C0 + a (kk + 4r), columns C0 + b (m16)
@@ -229,31 +242,38 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
           if (J == Q) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const int a = kk + 4 * r - C0, b = m16 - C0;
-              if (a >= 0 && a < 8 && b >= 0 && b <= a) band_st(8 * p + a, a - b, tile[SL * 8 + J][r]);
+              const int a = kk + 4 * r - C0, bq = m16 - C0;
+              if (a >= 0 && a < 8 && bq >= 0 && bq <= a) band_st(8 * p + a, a - bq, tile[J][r]);
             }
           }
         });
-        double myscal = 0.0;  // scal of this lane's column's reflector (lanes of the panel)
+        // per lane of panel column c: its reflector's scal and beta (set in step c)
+        double myscal = 0.0, mybeta = 0.0;
         sfor<8>([&](auto ii) {
           constexpr int i = decltype(ii)::value, CC_ = C0 + i;
           // pivot row rho = r0 + i: tile q0, row-in-tile 8 (1 - H) + i = kk + 4 r
           constexpr int PR = 8 * (1 - H) + i, GI = PR & 3, RI = PR >> 2;
           // x . x below the pivot, per lane for its own column, then over the 4 row groups
-          double xx = 0.0, alpha = 0.0;
+          double xx = 0.0, xx2 = 0.0, alpha = 0.0;
           sfor<8>([&](auto JJ) {
             constexpr int J = decltype(JJ)::value;
-            if (J >= q0) {
+            if (J > q0) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const double x = tile[SL * 8 + J][r];
-                const bool below = J > q0 || kk + 4 * r > PR;
-                xx = fma(below ? x : 0.0, below ? x : 0.0, xx);
+                const double x = tile[J][r];
+                if (r & 1) xx2 = fma(x, x, xx2);
+                else xx = fma(x, x, xx);
               }
-              if (J == q0) alpha = readlane_f64(tile[SL * 8 + J][RI], 16 * GI + CC_);
+            } else if (J == q0) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const double x = kk + 4 * r > PR ? tile[J][r] : 0.0;
+                xx = fma(x, x, xx);
+              }
+              alpha = readlane_f64(tile[J][RI], 16 * GI + CC_);
             }
           });
-          xx = swap_add_f64<32>(swap_add_f64<16>(xx));
+          xx = swap_add_f64<32>(swap_add_f64<16>(xx + xx2));
           const double xxp = readlane_f64(xx, CC_);
           // dlarfg (rcp/rsq refined to ~1 ulp); H = I when x = 0
           const double a2 = fma(alpha, alpha, xxp);
@@ -264,55 +284,64 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
           const double tau = nz ? (bt - alpha) * -copysign(rs, alpha) : 0.0;
           const double scal = nz ? rcp64(alpha - bt) : 0.0;
           const double amb = nz ? alpha - bt : 0.0;  // xt at the pivot: v = scal xt
-          if (m16 == CC_) myscal = scal;
-          // S'_c = sum over rows >= rho of xt(row) A(row, c), xt = column CC_ from lane CC_
-          // of the row (masked: 0 above the pivot, alpha - beta at it)
-          double S = 0.0;
-          auto xt_of = [&](int J, int r, double x) {
-            const int rr = kk + 4 * r;
-            return J > q0 ? x : (rr > PR ? x : rr == PR ? amb : 0.0);
-          };
+          if (m16 == CC_) {
+            myscal = scal;
+            mybeta = beta;
+          }
+          // S'_c = sum over rows >= rho of xt(row) A(row, c), xt = column CC_ from lane CC_ of
+          // the row: 0 above the pivot, alpha - beta at it, x below.  Tiles past q0 with one
+          // fused v_fmac_f64_dpp per register (volatile: the passes keep their order, and
+          // each opens with two wait states after the last VALU write of a DPP source).
+          double S = 0.0, S2 = 0.0;
+          dpp_fence();
           sfor<8>([&](auto JJ) {
             constexpr int J = decltype(JJ)::value;
-            if (J >= q0) {
+            if (J > q0) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const double xs = xt_of(J, r, rbcast<CC_>(tile[SL * 8 + J][r]));
-                S = fma(xs, tile[SL * 8 + J][r], S);
+                if (r & 1) S2 = fmac_row_v<CC_>(S2, tile[J][r], tile[J][r]);
+                else S = fmac_row_v<CC_>(S, tile[J][r], tile[J][r]);
               }
             }
           });
-          S = swap_add_f64<32>(swap_add_f64<16>(S));
+          double Sq = 0.0;
+          sfor<8>([&](auto JJ) {
+            constexpr int J = decltype(JJ)::value;
+            if (J == q0) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int rr = kk + 4 * r;
+                const double xb = rbcast<CC_>(tile[J][r]);
+                const double xs = rr > PR ? xb : rr == PR ? amb : 0.0;
+                Sq = fma(xs, tile[J][r], Sq);
+              }
+            }
+          });
+          S = swap_add_f64<32>(swap_add_f64<16>((S + S2) + Sq));
           // v^T A(:, c) = scal S'_c.  Columns c > CC_ of the panel: A(:, c) -= tau v (v^T A(:,c))
           // = tau scal^2 S'_c xt; the earlier columns c < CC_ keep x_c = v_c / scal_c below
           // their pivots, so their S'_c give the Gram entries v_c^T v_i = scal_c scal S'_c.
           const bool upd = m16 > CC_ && m16 < C0 + 8;
           const double gam = upd ? tau * scal * scal * S : 0.0;
-          // the R entries of column CC_ (rows r0 .. rho - 1 and beta at rho) and V column i,
-          // before the update (which leaves column CC_ itself unchanged)
           sfor<8>([&](auto JJ) {
             constexpr int J = decltype(JJ)::value;
-            if (J >= q0) {
+            if (J == q0) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const int rr = kk + 4 * r, row = 16 * J + rr;
-                const double x = tile[SL * 8 + J][r];
-                if (m16 == CC_ && row >= r0) {
-                  if (J == q0 && rr <= PR)  // rows r0 .. rho of R
-                    band_st(row, row - 8 * p - i, rr == PR ? beta : x);
-                  Vb[row - r0][i] = J > q0 || rr > PR ? x * scal : rr == PR ? 1.0 : 0.0;
-                }
+                const int rr = kk + 4 * r;
+                const double xb = rbcast<CC_>(tile[J][r]);
+                const double xs = rr > PR ? xb : rr == PR ? amb : 0.0;
+                tile[J][r] = fma(-gam, xs, tile[J][r]);
               }
             }
           });
+          dpp_fence();
           sfor<8>([&](auto JJ) {
             constexpr int J = decltype(JJ)::value;
-            if (J >= q0) {
+            if (J > q0) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const double xs = xt_of(J, r, rbcast<CC_>(tile[SL * 8 + J][r]));
-                tile[SL * 8 + J][r] = fma(-gam, xs, tile[SL * 8 + J][r]);
-              }
+              for (int r = 0; r < 4; ++r)
+                tile[J][r] = fnmac_row_v<CC_>(tile[J][r], tile[J][r], gam);
             }
           });
           // T column i: T[i][i] = tau; T[j][i] = -tau sum_{k=j}^{i-1} T[j][k] t_k,
@@ -331,14 +360,34 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
             if (kk == 0 && jl > i && jl < 8) sm.u.s.T[jl * 8 + i] = 0.0;
           }
         });
+        // V (column c = m16 - C0: scal_c x below its pivot, 1 at it, 0 above) and the R entries
+        // (rows r0 .. r0 + c - 1 as updated, beta_c at the pivot): the panel columns hold x_c
+        // below their pivots (a step leaves its own column unchanged).  V rows r0 - 8 .. r0 - 1
+        // (tile q0 above the panel when H = 0) land in V's unused rows 120..127.
+        {
+          const int cl = m16 - C0;
+          const bool pc = cl >= 0 && cl < 8;
+          const int prc = 8 * (1 - H) + cl;  // the column's pivot row within tile q0
+          sfor<8>([&](auto JJ) {
+            constexpr int J = decltype(JJ)::value;
+            if (J >= q0) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int rr = kk + 4 * r, row = 16 * J + rr;
+                const double x = tile[J][r];
+                const bool below = J > q0 || rr > prc;
+                const double vv = below ? x * myscal : (J == q0 && rr == prc ? 1.0 : 0.0);
+                if (pc) Vb[(row - r0) & 127][cl] = vv;
+                if (pc && J == q0 && rr >= 8 * (1 - H) && rr <= prc)
+                  band_st(row, row - 8 * p - cl, rr == prc ? mybeta : x);
+              }
+            }
+          });
+        }
       };
-      if (Q == I0) {
-        if (h == 0) qr(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-        else qr(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
-      } else {
-        if (h == 0) qr(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
-        else qr(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
-      }
+      if (h == 0) qr(std::integral_constant<int, 0>{});
+      else qr(std::integral_constant<int, 1>{});
+      if (swp) swap_slots();
       // V rows of the panel's top block above the diagonal and the rows of the trailing
       // columns are written above; the record gets V and T
       const int m = 128 - r0;
