@@ -89,7 +89,7 @@ static_assert(BandRec::pv(15) == BandRec::PT, "panel reflector offsets");
 // the chase schedule (scripts/two_stage_b8.py: schedule): tasks of sweep j, their first index,
 // and the round in which sweep j starts (two slots, sweep j+1 three tasks behind sweep j)
 struct ChasePlan {
-  short start[126], first[127], ntask[126];
+  int start[126], first[127], ntask[126];  // 32-bit: scalar loads
   int rounds;
 };
 __host__ __device__ constexpr int chase_ntask(int j) { return j <= 125 ? (125 - j) / 8 + 1 : 0; }
@@ -100,13 +100,13 @@ __host__ __device__ constexpr ChasePlan make_chase_plan() {
     int s = 0;
     if (j >= 1 && p.start[j - 1] + 3 > s) s = p.start[j - 1] + 3;
     if (j >= 2 && p.start[j - 2] + p.ntask[j - 2] > s) s = p.start[j - 2] + p.ntask[j - 2];
-    p.start[j] = (short)s;
-    p.ntask[j] = (short)chase_ntask(j);
-    p.first[j] = (short)acc;
+    p.start[j] = s;
+    p.ntask[j] = chase_ntask(j);
+    p.first[j] = acc;
     acc += p.ntask[j];
     if (s + p.ntask[j] > end) end = s + p.ntask[j];
   }
-  p.first[126] = (short)acc;
+  p.first[126] = acc;
   p.rounds = end;
   return p;
 }

@@ -145,10 +145,15 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
       }
     };
     diag(tile9[0], I0);
-    // (the select keeps tile9's index static)
+    // (selects, not branches on t: see pick below)
+    sfor<NTW - 1>([&](auto tt) {
+      constexpr int t = decltype(tt)::value + 1;
+      f64x4 d = tile9[t];
+      diag(d, I1);
+      const bool on = t == 8 - wave;
 #pragma unroll
-    for (int t = 1; t < NTW; ++t)
-      if (t == 8 - wave) diag(tile9[t], I1);
+      for (int r = 0; r < 4; ++r) tile9[t][r] = on ? d[r] + 0.0 : tile9[t][r] + 0.0;
+    });
   }
 
   // ---- the full symmetric A: upper tiles as transposes of the lower ones, through LDS -----
@@ -164,28 +169,35 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
   }
   __syncthreads();
   // tile[s * 8 + J] = A(rows 16J + kk + 4r, columns 16 I_s + m16), I_0 = w, I_1 = 7 - w
+  // (value selects throughout: per-wave branches that each copy a different tile get merged
+  // into one copy through a pointer phi, which moves the tiles to scratch memory)
   f64x4 tile[16];
-  auto build = [&](auto W_) {
-    constexpr int W = decltype(W_)::value;
-    sfor<16>([&](auto tt) {
-      constexpr int t = decltype(tt)::value;
-      constexpr int I = t < 8 ? W : 7 - W, J = t & 7;
-      if constexpr (J >= I) {
-        constexpr int t9 = t < 8 ? J - W : (8 - W) + J - (7 - W);
-        tile[t] = tile9[t9];
-      } else {  // (J, I) = (I, J)^T: element (a, b) of (J, I) is (b, a) of (I, J)
-        const double *s = sm.u.mir[mir_slot(I, J)];
+  sfor<16>([&](auto tt) {
+    constexpr int t = decltype(tt)::value, J = t & 7;
+    const int I = t < 8 ? I0 : I1;
+    // (J, I), J >= I, from tile9: slot 0 at t9 = J - w, slot 1 at t9 = J + 1
+    f64x4 own;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) tile[t][r] = s[m16 * 17 + kk + 4 * r];
+    for (int r = 0; r < 4; ++r) {
+      if constexpr (t < 8) {
+        long long bits = 0;
+        sfor<4>([&](auto WW) {
+          constexpr int W = decltype(WW)::value;
+          if constexpr (J >= W) bits |= __double_as_longlong(tile9[J - W][r]) & -(long long)(wave == W);
+        });
+        own[r] = __longlong_as_double(bits);
+      } else {
+        own[r] = tile9[J + 1][r];
       }
-    });
-  };
-  switch (wave) {
-    case 0: build(std::integral_constant<int, 0>{}); break;
-    case 1: build(std::integral_constant<int, 1>{}); break;
-    case 2: build(std::integral_constant<int, 2>{}); break;
-    default: build(std::integral_constant<int, 3>{}); break;
-  }
+    }
+    // (J, I) = (I, J)^T for J < I: element (a, b) of (J, I) is (b, a) of (I, J)
+    const double *s = sm.u.mir[J < I ? mir_slot(I, J) : 0];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double mv = s[m16 * 17 + kk + 4 * r];
+      tile[t][r] = J >= I ? own[r] + 0.0 : mv + 0.0;
+    }
+  });
   // x' and b1 (fp64); xb_mean in the reference's sequential fp32 order (:671)
   float xbm;
   {
@@ -232,21 +244,39 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
         });
       };
       if (swp) swap_slots();
+      // tile (j, Q) of slot 0 by value: bit masks, not branches — branches that each touch a
+      // different tile get merged into one access through a pointer phi, and that sends the
+      // whole slot to scratch memory
+      auto pick = [&](int j) {
+        f64x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          long long bits = 0;
+          sfor<8>([&](auto JJ) {
+            constexpr int J = decltype(JJ)::value;
+            bits |= __double_as_longlong(tile[J][r]) & -(long long)(j == J);
+          });
+          o[r] = __longlong_as_double(bits);
+        }
+        return o;
+      };
       auto qr = [&](auto H_) {
         constexpr int H = decltype(H_)::value;
         constexpr int C0 = 8 * H;
+        // the pivot tile (q0, Q): the panel's rows r0 - 8 + 8H .. ; the QR changes only the
+        // panel's columns, which no later step reads, so neither it nor the tiles below it are
+        // written back
+        f64x4 tq = pick(q0);
         // band: the diagonal block D_p (rows 8p + a, columns 8p + b, b <= a): tile (Q, Q),
         // rows C0 + a (kk + 4r), columns C0 + b (m16)
-        sfor<8>([&](auto JJ) {
-          constexpr int J = decltype(JJ)::value;
-          if (J == Q) {
+        {
+          const f64x4 td = H == 0 ? tq : pick(Q);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int a = kk + 4 * r - C0, bq = m16 - C0;
-              if (a >= 0 && a < 8 && bq >= 0 && bq <= a) band_st(8 * p + a, a - bq, tile[J][r]);
-            }
+          for (int r = 0; r < 4; ++r) {
+            const int a = kk + 4 * r - C0, bq = m16 - C0;
+            if (a >= 0 && a < 8 && bq >= 0 && bq <= a) band_st(8 * p + a, a - bq, td[r]);
           }
-        });
+        }
         // per lane of panel column c: its reflector's scal and beta (set in step c)
         double myscal = 0.0, mybeta = 0.0;
         sfor<8>([&](auto ii) {
@@ -254,7 +284,7 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
           // pivot row rho = r0 + i: tile q0, row-in-tile 8 (1 - H) + i = kk + 4 r
           constexpr int PR = 8 * (1 - H) + i, GI = PR & 3, RI = PR >> 2;
           // x . x below the pivot, per lane for its own column, then over the 4 row groups
-          double xx = 0.0, xx2 = 0.0, alpha = 0.0;
+          double xx = 0.0, xx2 = 0.0;
           sfor<8>([&](auto JJ) {
             constexpr int J = decltype(JJ)::value;
             if (J > q0) {
@@ -264,15 +294,14 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
                 if (r & 1) xx2 = fma(x, x, xx2);
                 else xx = fma(x, x, xx);
               }
-            } else if (J == q0) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const double x = kk + 4 * r > PR ? tile[J][r] : 0.0;
-                xx = fma(x, x, xx);
-              }
-              alpha = readlane_f64(tile[J][RI], 16 * GI + CC_);
             }
           });
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double x = kk + 4 * r > PR ? tq[r] : 0.0;
+            xx = fma(x, x, xx);
+          }
+          const double alpha = readlane_f64(tq[RI], 16 * GI + CC_);
           xx = swap_add_f64<32>(swap_add_f64<16>(xx + xx2));
           const double xxp = readlane_f64(xx, CC_);
           // dlarfg (rcp/rsq refined to ~1 ulp); H = I when x = 0
@@ -305,36 +334,22 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
             }
           });
           double Sq = 0.0;
-          sfor<8>([&](auto JJ) {
-            constexpr int J = decltype(JJ)::value;
-            if (J == q0) {
+          double xsq[4];
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int rr = kk + 4 * r;
-                const double xb = rbcast<CC_>(tile[J][r]);
-                const double xs = rr > PR ? xb : rr == PR ? amb : 0.0;
-                Sq = fma(xs, tile[J][r], Sq);
-              }
-            }
-          });
+          for (int r = 0; r < 4; ++r) {
+            const int rr = kk + 4 * r;
+            const double xb = rbcast<CC_>(tq[r]);
+            xsq[r] = rr > PR ? xb : rr == PR ? amb : 0.0;
+            Sq = fma(xsq[r], tq[r], Sq);
+          }
           S = swap_add_f64<32>(swap_add_f64<16>((S + S2) + Sq));
           // v^T A(:, c) = scal S'_c.  Columns c > CC_ of the panel: A(:, c) -= tau v (v^T A(:,c))
           // = tau scal^2 S'_c xt; the earlier columns c < CC_ keep x_c = v_c / scal_c below
           // their pivots, so their S'_c give the Gram entries v_c^T v_i = scal_c scal S'_c.
           const bool upd = m16 > CC_ && m16 < C0 + 8;
           const double gam = upd ? tau * scal * scal * S : 0.0;
-          sfor<8>([&](auto JJ) {
-            constexpr int J = decltype(JJ)::value;
-            if (J == q0) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int rr = kk + 4 * r;
-                const double xb = rbcast<CC_>(tile[J][r]);
-                const double xs = rr > PR ? xb : rr == PR ? amb : 0.0;
-                tile[J][r] = fma(-gam, xs, tile[J][r]);
-              }
-            }
-          });
+          for (int r = 0; r < 4; ++r) tq[r] = fma(-gam, xsq[r], tq[r]);
           dpp_fence();
           sfor<8>([&](auto JJ) {
             constexpr int J = decltype(JJ)::value;
@@ -368,18 +383,22 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
           const int cl = m16 - C0;
           const bool pc = cl >= 0 && cl < 8;
           const int prc = 8 * (1 - H) + cl;  // the column's pivot row within tile q0
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {  // the pivot tile
+            const int rr = kk + 4 * r, row = 16 * q0 + rr;
+            const double x = tq[r];
+            const double vv = rr > prc ? x * myscal : (rr == prc ? 1.0 : 0.0);
+            if (pc) Vb[(row - r0) & 127][cl] = vv;
+            if (pc && rr >= 8 * (1 - H) && rr <= prc)
+              band_st(row, row - 8 * p - cl, rr == prc ? mybeta : x);
+          }
           sfor<8>([&](auto JJ) {
             constexpr int J = decltype(JJ)::value;
-            if (J >= q0) {
+            if (J > q0) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const int rr = kk + 4 * r, row = 16 * J + rr;
-                const double x = tile[J][r];
-                const bool below = J > q0 || rr > prc;
-                const double vv = below ? x * myscal : (J == q0 && rr == prc ? 1.0 : 0.0);
-                if (pc) Vb[(row - r0) & 127][cl] = vv;
-                if (pc && J == q0 && rr >= 8 * (1 - H) && rr <= prc)
-                  band_st(row, row - 8 * p - cl, rr == prc ? mybeta : x);
+                const int row = 16 * J + kk + 4 * r;
+                if (pc) Vb[row - r0][cl] = tile[J][r] * myscal;
               }
             }
           });

@@ -83,10 +83,20 @@ band_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts, double *__
   // per-lane static part of the store masks: the diagonal block stores its lower triangle
   const unsigned smask = rB ? (2u << b) - 1u : 0xffu;
   const int trash = 16 * 128 + 16 * (l & 7);  // a padding row of this lane
-  int js = slot;  // this slot's sweep, its start round, first task index and task count
-  int st = cChase.start[js], fj = cChase.first[js], ntj = cChase.ntask[js];
+  // each slot's sweep, its start round, first task index and task count: uniform values (both
+  // slots, scalar loads of the plan), so no vector load keeps the round loop waiting on memory
+  int jsS[2], stS[2], fjS[2], ntS[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    jsS[s] = s;
+    stS[s] = cChase.start[s];
+    fjS[s] = cChase.first[s];
+    ntS[s] = cChase.ntask[s];
+  }
   double *__restrict__ r2 = rec + HR::R2;
   for (int R = 0; R < cChase.rounds; ++R) {
+    const int js = slot ? jsS[1] : jsS[0], st = slot ? stS[1] : stS[0];
+    const int fj = slot ? fjS[1] : fjS[0], ntj = slot ? ntS[1] : ntS[0];
     const int t = R - st;
     const bool act = js <= 125 && t >= 0 && t < ntj;
     const int r = act ? js + 1 + 8 * t : 0;  // the task's first row (inactive: row 0)
@@ -138,11 +148,14 @@ band_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts, double *__
     for (int e = 0; e < 8; ++e) band[(m >> e) & 1u ? baseX + off[e] : trash + e] = X[e];
     if (act && rA && lo < L) band[acol] = lo == 0 ? beta : 0.0;
     if (act && rA) r2[(fj + t) * 8 + lo] = lo == 0 ? tau : (lo < L ? v : 0.0);
-    if (act && t + 1 == ntj) {  // this slot's next sweep
-      fj += ntj + chase_ntask(js + 1);
-      js += 2;
-      st = js <= 125 ? cChase.start[js] : 1 << 30;
-      ntj = chase_ntask(js);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {  // a slot whose sweep ends this round takes the next one
+      if (jsS[s] <= 125 && R - stS[s] + 1 == ntS[s]) {
+        fjS[s] += ntS[s] + chase_ntask(jsS[s] + 1);
+        jsS[s] += 2;
+        stS[s] = jsS[s] <= 125 ? cChase.start[jsS[s]] : 1 << 30;
+        ntS[s] = chase_ntask(jsS[s]);
+      }
     }
     __syncthreads();
   }
