@@ -9,20 +9,23 @@ __constant__ ChasePlan cChase = kChase;
 
 // ==== stage 2: chase, quadrature, back-transform, epilogue ===================================
 struct BandTailSmem {
-  static constexpr int ROWS = 136;  // 128 rows + 8 padding rows (reads past the matrix land
-                                    // here; stores that a lane must not make go to row 128+)
+  static constexpr int ROWS = 142;  // 128 rows + padding: a task at row r <= 126 reaches row
+                                    // r + 15; what lands past row 127 is never read as data
+  static constexpr int UROWS = 136; // u rows r + e <= 133
   union {
     double band[ROWS * 16];  // the chase: A(i, i - d) at 16 i + d, d = 0..15
     double tq[129][4];       // then d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
     double y[128];           // then y for the back-transform
   } a;
   union {
-    double u[2][128];      // Q1^T b1, Q1^T x' through the chase's reflectors
+    double u[2][UROWS];  // Q1^T b1, Q1^T x', then through the chase's reflectors
     struct {
       double Ym[128], Zm[128];  // quadrature sum / exact solve, walk order
     } q;
   } b;
 };
+// (8 blocks of one wavefront per CU: the chase is issue-bound at two waves per SIMD)
+static_assert(8 * sizeof(BandTailSmem) <= 160 * 1024, "band tail LDS");
 
 __global__ void __launch_bounds__(64, 2)
 band_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts, double *__restrict__ ws,
@@ -58,31 +61,43 @@ band_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts, double *__
     const int i = e >> 4, d = e & 15;
     band[e] = i < 128 && d <= HR::B ? rec[HR::BAND + i * (HR::B + 1) + d] : 0.0;
   }
-  sm.b.u[0][l] = rec[HR::U1 + l];
-  sm.b.u[0][64 + l] = rec[HR::U1 + 64 + l];
-  sm.b.u[1][l] = rec[HR::U2 + l];
-  sm.b.u[1][64 + l] = rec[HR::U2 + 64 + l];
+  for (int i = l; i < BandTailSmem::UROWS; i += 64) {
+    sm.b.u[0][i] = i < 128 ? rec[HR::U1 + i] : 0.0;
+    sm.b.u[1][i] = i < 128 ? rec[HR::U2 + i] : 0.0;
+  }
   __syncthreads();
 
   // ---- the chase: rounds of up to two tasks (slot 0: even sweeps, slot 1: odd sweeps) ------
-  // Lanes of a slot: row 0 = lanes 0-7 the left block's columns (and the reflector: v_e on
-  // lane e), lanes 8-15 the diagonal block's rows; row 1 = lanes 0-7 the bulge rows below (v
-  // again on lanes 0-7), lanes 8-15 idle.  Every lane holds one 8-vector X of its block at the
-  // LDS words 16 r + base + off[e] (r: the task's first row): the left block's column
-  // r - 7 + lo at rows r + e (off 17 e + 7 - lo), the diagonal block's row r + b in both
-  // triangles (off 16 max(e, b) + |e - b|), the bulge row r + 8 + lo (off 16 (8 + lo) + 8 + lo
-  // - e).  One instruction stream for all: X -= al v + be w with (al, be) = (tau v^T X, 0)
-  // one-sided and (w_b, v_b) two-sided (w = tau (D v) - 1/2 tau^2 (v^T D v) v).
+  // The reflector of a task (rows r .. r + L - 1) is v_e on lanes e = 0..7 of both 16-lane rows
+  // of its slot.  Every lane holds one 8-vector X at the LDS words M r + C + off[e]:
+  //   row 0, lanes 0-6:  the left block's column r - 7 + lo at rows r + e (16 r + 7 - lo + 17 e)
+  //   row 0, lane 7:     u1 rows r + e
+  //   row 0, lanes 8-15: the diagonal block's row r + b, both triangles
+  //                      (16 r + 16 max(e, b) + |e - b|)
+  //   row 1, lanes 0-7:  the bulge row r + 8 + lo (16 (r + 8 + lo) + 8 + lo - e)
+  //   row 1, lanes 8-15: u2 rows r + e (eight identical copies)
+  // One instruction stream for all: X -= al v + be w with (al, be) = (tau v^T X, 0) one-sided
+  // and (w_b, v_b) two-sided (w = tau (D v) - 1/2 tau^2 (v^T D v) v).  Every lane stores all 8
+  // entries back: what lies past row 127 (or is the identity's zero left of a sweep's first
+  // task) is rewritten harmlessly (v_e = 0 there, values stay finite); an entry of the
+  // diagonal block held twice (lanes 8 + b and 8 + e) takes the later store's rounding; the
+  // annihilated column is written last.  A slot without a task this round repeats the other
+  // slot's task (identical values to identical words).
   const int slot = l >> 5, rr = (l >> 4) & 1, lo = l & 15;
   const int e8 = lo & 7, b = lo - 8;
-  const bool rA = rr == 0 && lo < 8, rB = rr == 0 && lo >= 8, rC = rr == 1 && lo < 8;
-  int off[8];
+  const int U1 = (int)(sm.b.u[0] - band), U2 = (int)(sm.b.u[1] - band);
+  int M, CO[8];  // words: M r + CO[e]
+  {
+    const bool rA = rr == 0 && lo < 7, rB = rr == 0 && lo >= 8, rC = rr == 1 && lo < 8;
+    M = rA || rB || rC ? 16 : 1;
 #pragma unroll
-  for (int e = 0; e < 8; ++e)
-    off[e] = rA ? 17 * e : rB ? 16 * max(e, b) + (e > b ? e - b : b - e) : -e;
-  // per-lane static part of the store masks: the diagonal block stores its lower triangle
-  const unsigned smask = rB ? (2u << b) - 1u : 0xffu;
-  const int trash = 16 * 128 + 16 * (l & 7);  // a padding row of this lane
+    for (int e = 0; e < 8; ++e)
+      CO[e] = rA ? 7 - lo + 17 * e
+            : rB ? 16 * max(e, b) + (e > b ? e - b : b - e)
+            : rC ? 136 + 17 * lo - e
+            : (rr == 0 ? U1 : U2) + e;
+  }
+  const bool rV = rr == 0 && lo < 8;  // stores the reflector
   // each slot's sweep, its start round, first task index and task count: uniform values (both
   // slots, scalar loads of the plan), so no vector load keeps the round loop waiting on memory
   int jsS[2], stS[2], fjS[2], ntS[2];
@@ -95,59 +110,64 @@ band_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts, double *__
   }
   double *__restrict__ r2 = rec + HR::R2;
   for (int R = 0; R < cChase.rounds; ++R) {
-    const int js = slot ? jsS[1] : jsS[0], st = slot ? stS[1] : stS[0];
-    const int fj = slot ? fjS[1] : fjS[0], ntj = slot ? ntS[1] : ntS[0];
-    const int t = R - st;
-    const bool act = js <= 125 && t >= 0 && t < ntj;
-    const int r = act ? js + 1 + 8 * t : 0;  // the task's first row (inactive: row 0)
-    const int L = min(8, 128 - r);           // reflector length
-    const bool t0 = t == 0;
-    // the annihilated column: rows r + e, column r - 8 (t > 0) or r - 1 (t = 0)
-    const int acol = 16 * r + 17 * e8 + (t0 ? 1 : 8);
-    double xe = band[acol];
-    xe = act && lo < 8 && e8 < L ? xe : 0.0;
-    const double xx = rbcast<0>(rsum8(e8 >= 1 ? xe * xe : 0.0));
-    const double alpha = rbcast<0>(xe);
-    // this lane's vector (loaded while the reflector is formed)
-    const int rowC = min(r + 8 + lo, 135);
-    const int baseX = rA ? 16 * r + 7 - lo : rB ? 16 * r : 16 * rowC + 8 + lo;
-    double X[8];
+    // per slot (uniform): task row, annihilated-column word, reflector index
+    int rS[2], aS[2], qS[2];
+    bool actS[2];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) X[e] = band[baseX + off[e]];
-    const double a2 = fma(alpha, alpha, xx);
-    const double rs = rsq64(a2);
-    const bool nz = xx > 0.0;
-    const double bt = -copysign(a2 * rs, alpha);
-    const double beta = nz ? bt : alpha;
-    const double tau = nz ? (bt - alpha) * -copysign(rs, alpha) : 0.0;
-    const double scal = nz ? rcp64(alpha - bt) : 0.0;
-    double v = lo < 8 ? (e8 == 0 ? 1.0 : xe * scal) : 0.0;  // v_e on lanes e of a row
-    dpp_pin(v);
-    double dot = 0.0, dot2 = 0.0;  // v^T X (two chains)
-    sfor<8>([&](auto ee) {
-      constexpr int e = decltype(ee)::value;
-      if constexpr (e % 2 == 0) dot = fmac_row<e>(dot, v, X[e]);
-      else dot2 = fmac_row<e>(dot2, v, X[e]);
-    });
-    dot += dot2;
-    const double vb = ror8(v);  // v_b on lane 8 + b
-    const double s1 = rsum8(vb * dot);
-    double wB = tau * fma(-0.5 * tau, s1 * vb, dot);
-    const double al = rB ? wB : tau * dot;
-    const double be = rB ? vb : 0.0;
-    dpp_pin(wB);
-    sfor<8>([&](auto ee) {
-      constexpr int e = decltype(ee)::value;
-      X[e] = fnmac_row<8 + e>(fnmac_row<e>(X[e], v, al), wB, be);
-    });
-    // stores (the ones a lane must not make go to its padding row): the blocks, the
-    // annihilated column, the reflector
-    const bool okA = rA && !t0 && lo < 7, okB = rB && b < L, okC = rC && r + 8 + lo < 128 && L == 8;
-    const unsigned m = act && (okA || okB || okC) ? smask & (okC ? 0xffu : (1u << L) - 1u) : 0u;
+    for (int s = 0; s < 2; ++s) {
+      const int t = R - stS[s];
+      actS[s] = jsS[s] <= 125 && t >= 0 && t < ntS[s];
+      rS[s] = jsS[s] + 1 + 8 * t;
+      aS[s] = 16 * rS[s] + (t == 0 ? 1 : 8);
+      qS[s] = fjS[s] + t;
+    }
+    if (actS[0] || actS[1]) {
+      // a slot without a task repeats the other's
+      const int sl = actS[slot] ? slot : slot ^ 1;
+      const int r = sl ? rS[1] : rS[0];
+      const int acol = (sl ? aS[1] : aS[0]) + 17 * e8;  // rows r + e8 of the annihilated column
+      const int q = sl ? qS[1] : qS[0];
+      double xe = band[acol];
+      xe = r + e8 < 128 ? xe : 0.0;
+      const double xx = rbcast<0>(rsum8(e8 >= 1 ? xe * xe : 0.0));
+      const double alpha = rbcast<0>(xe);
+      // this lane's vector (loaded while the reflector is formed)
+      const int mr = M * r;
+      double X[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) band[(m >> e) & 1u ? baseX + off[e] : trash + e] = X[e];
-    if (act && rA && lo < L) band[acol] = lo == 0 ? beta : 0.0;
-    if (act && rA) r2[(fj + t) * 8 + lo] = lo == 0 ? tau : (lo < L ? v : 0.0);
+      for (int e = 0; e < 8; ++e) X[e] = band[mr + CO[e]];
+      const double a2 = fma(alpha, alpha, xx);
+      const double rs = rsq64(a2);
+      const bool nz = xx > 0.0;
+      const double bt = -copysign(a2 * rs, alpha);
+      const double beta = nz ? bt : alpha;
+      const double tau = nz ? (bt - alpha) * -copysign(rs, alpha) : 0.0;
+      const double scal = nz ? rcp64(alpha - bt) : 0.0;
+      double v = e8 == 0 ? 1.0 : xe * scal;  // v_e on lanes e of a row (lanes 8-15: unused)
+      dpp_pin(v);
+      double dot = 0.0, dot2 = 0.0;  // v^T X (two chains)
+      sfor<8>([&](auto ee) {
+        constexpr int e = decltype(ee)::value;
+        if constexpr (e % 2 == 0) dot = fmac_row<e>(dot, v, X[e]);
+        else dot2 = fmac_row<e>(dot2, v, X[e]);
+      });
+      dot += dot2;
+      const double vb = ror8(v);  // v_b on lane 8 + b
+      const double s1 = rsum8(vb * dot);
+      double wB = tau * fma(-0.5 * tau, s1 * vb, dot);
+      const bool twos = rr == 0 && lo >= 8;
+      const double al = twos ? wB : tau * dot;
+      const double be = twos ? vb : 0.0;
+      dpp_pin(wB);
+      sfor<8>([&](auto ee) {
+        constexpr int e = decltype(ee)::value;
+        X[e] = fnmac_row<8 + e>(fnmac_row<e>(X[e], v, al), wB, be);
+      });
+#pragma unroll
+      for (int e = 0; e < 8; ++e) band[mr + CO[e]] = X[e];
+      band[acol] = e8 == 0 ? beta : 0.0;
+      if (rV) r2[q * 8 + lo] = lo == 0 ? tau : v;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {  // a slot whose sweep ends this round takes the next one
       if (jsS[s] <= 125 && R - stS[s] + 1 == ntS[s]) {
@@ -168,31 +188,7 @@ band_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts, double *__
   sm.a.tq[64 + l][0] = dB;
   sm.a.tq[64 + l][1] = eB;
   if (l == 0) sm.a.tq[KP][1] = 0.0;
-  // ---- Q2^T applied to u1, u2: sweep after sweep, a sweep's reflectors (disjoint rows) 8 at a
-  // time: lane = reflector tt (l >> 3) + 8 pass, entry e = l & 7
-  auto apply_sweep = [&](double *u0, double *u1v, int j, int pass, bool both) {
-    const int tt = 8 * pass + (l >> 3), e = l & 7;
-    const bool ok = tt < cChase.ntask[j];
-    const int r = j + 1 + 8 * tt;
-    const int L = min(8, 128 - r);
-    const double *q = r2 + (ok ? cChase.first[j] + tt : 0) * 8;
-    const double tu = ok ? q[0] : 0.0;
-    const double ve = ok && e < L ? (e == 0 ? 1.0 : q[e]) : 0.0;
-    const int row = ok && e < L ? r + e : 0;
-    const double a0 = ve * u0[row];
-    const double d0 = rsum8(a0);
-    double d1 = 0.0;
-    if (both) d1 = rsum8(ve * u1v[row]);
-    __syncthreads();
-    if (ok && e < L) {
-      u0[row] = fma(-tu * d0, ve, u0[row]);
-      if (both) u1v[row] = fma(-tu * d1, ve, u1v[row]);
-    }
-    __syncthreads();
-  };
-  for (int j = 0; j < 126; ++j)
-    for (int pass = 0; 8 * pass < cChase.ntask[j]; ++pass)
-      apply_sweep(sm.b.u[0], sm.b.u[1], j, pass, true);
+  // (Q2^T u1, Q2^T u2 were formed in the chase)
   sm.a.tq[l][2] = sm.b.u[0][l];
   sm.a.tq[64 + l][2] = sm.b.u[0][64 + l];
   sm.a.tq[l][3] = sm.b.u[1][l];
@@ -286,39 +282,95 @@ band_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts, double *__
   sm.a.y[l] = y0;
   sm.a.y[64 + l] = y1;
   __syncthreads();
-  for (int j = 125; j >= 0; --j)
-    for (int pass = 0; 8 * pass < cChase.ntask[j]; ++pass)
-      apply_sweep(sm.a.y, nullptr, j, pass, false);
+  {
+    // sweeps in reverse; a sweep's reflectors act on disjoint rows, 8 per pass (lane: reflector
+    // l >> 3, entry l & 7); the next pass's reflectors are loaded while this one runs
+    // (the loads are unconditional, at a valid address, and masked at use: loads under a
+    // branch would make the wait before the use cover the prefetch too)
+    struct Pass {
+      double tu, ve;  // raw: q[0], q[e]
+      int row;        // -1: no entry
+    };
+    auto load_pass = [&](int j, int pass) {
+      Pass d;
+      const int tt = 8 * pass + (l >> 3), e = l & 7;
+      const bool ok = j >= 0 && tt < chase_ntask(j);
+      const int r = j + 1 + 8 * tt;
+      const bool in = ok && e < min(8, 128 - r);
+      const double *q = r2 + (ok ? cChase.first[max(j, 0)] + tt : 0) * 8;
+      d.tu = q[0];
+      d.ve = q[e];
+      d.row = in ? r + e : -1;
+      return d;
+    };
+    int j = 125, pass = 0;
+    Pass cur = load_pass(j, pass);
+    while (j >= 0) {
+      int jn = j, pn = pass + 1;
+      if (8 * pn >= chase_ntask(j)) {
+        jn = j - 1;
+        pn = 0;
+      }
+      const Pass nxt = load_pass(jn, pn);
+      const bool in = cur.row >= 0;
+      const double ve = in ? ((l & 7) == 0 ? 1.0 : cur.ve) : 0.0;
+      const double yv = sm.a.y[in ? cur.row : 0];
+      const double dd = rsum8(ve * yv);
+      if (in) sm.a.y[cur.row] = fma(-cur.tu * dd, ve, yv);
+      __syncthreads();
+      cur = nxt;
+      j = jn;
+      pass = pn;
+    }
+  }
   y0 = sm.a.y[l];
   y1 = sm.a.y[64 + l];
-  for (int p = HR::NP - 1; p >= 0; --p) {
-    const int r0 = 8 * p + 8, mrows = 128 - r0;
-    const double *pv = rec + HR::pv(p);
-    const double *pt = rec + HR::PT + 64 * p;
-    // lane l: rows l and 64 + l (row index >= r0 only)
-    const int ia = l - r0, ib = 64 + l - r0;
-    const bool va = ia >= 0 && ia < mrows, vb = ib >= 0 && ib < mrows;
-    double Va[8], Vbb[8], s[8];
+  {
+    // lane l: rows l and 64 + l of V_p (rows >= r0 only) and T_p[l >> 3][l & 7] (T upper, zeros
+    // below); the next panel's loads are issued before this one's arithmetic (unconditional, at
+    // valid addresses, masked at use)
+    struct Panel {
+      double Va[8], Vb[8], t;
+    };
+    auto load_panel = [&](int p) {
+      Panel d;
+      const int r0 = 8 * p + 8;
+      const double *pv = rec + HR::pv(p);
+      const int ia = max(l - r0, 0), ib = max(64 + l - r0, 0);
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      Va[a] = va ? pv[ia * 8 + a] : 0.0;
-      Vbb[a] = vb ? pv[ib * 8 + a] : 0.0;
-      s[a] = fma(Va[a], y0, Vbb[a] * y1);
-    }
-    wave_sum4_dpp(s[0], s[1], s[2], s[3]);
-    wave_sum4_dpp(s[4], s[5], s[6], s[7]);
-    double z[8];  // z = T s (T upper)
+      for (int a = 0; a < 8; ++a) {
+        d.Va[a] = pv[ia * 8 + a];
+        d.Vb[a] = pv[ib * 8 + a];
+      }
+      d.t = rec[HR::PT + 64 * p + l];
+      return d;
+    };
+    Panel cur = load_panel(HR::NP - 1);
+    for (int p = HR::NP - 1; p >= 0; --p) {
+      const Panel nxt = load_panel(max(p - 1, 0));
+      const int r0 = 8 * p + 8;
+      const bool va = l >= r0, vb = 64 + l >= r0;
+      double Va[8], Vbb[8], s[8];
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      double acc = 0.0;
+      for (int a = 0; a < 8; ++a) {
+        Va[a] = va ? cur.Va[a] : 0.0;
+        Vbb[a] = vb ? cur.Vb[a] : 0.0;
+        s[a] = fma(Va[a], y0, Vbb[a] * y1);
+      }
+      wave_sum4_dpp(s[0], s[1], s[2], s[3]);
+      wave_sum4_dpp(s[4], s[5], s[6], s[7]);
+      // z = T s: lane (a, b) forms T[a][b] s_b, the 8 lanes of row a sum it
+      double sb = s[0];
 #pragma unroll
-      for (int bq = a; bq < 8; ++bq) acc = fma(pt[a * 8 + bq], s[bq], acc);
-      z[a] = acc;
-    }
+      for (int b = 1; b < 8; ++b) sb = (l & 7) == b ? s[b] : sb;
+      const double zl = rsum8(cur.t * sb);
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      y0 = fma(-Va[a], z[a], y0);
-      y1 = fma(-Vbb[a], z[a], y1);
+      for (int a = 0; a < 8; ++a) {
+        const double za = readlane_f64(zl, 8 * a);
+        y0 = fma(-Va[a], za, y0);
+        y1 = fma(-Vbb[a], za, y1);
+      }
+      cur = nxt;
     }
   }
 

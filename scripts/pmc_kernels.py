@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise scripts/profile_r4.sh's rocprofv3 runs into profiles/pmc_kernels.json (read by
+"""Summarise scripts/profile_round.sh's rocprofv3 runs into profiles/pmc_kernels.json (read by
 bench.py's roofline) and profiles/<tag>_<config>_{kernel_stats.csv,kernels.json}.
 
 Per config and kernel (names as bench.py / cwbl_kernel_times give them):

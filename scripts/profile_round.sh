@@ -6,7 +6,7 @@
 # writes profiles/pmc_kernels.json and profiles/${TAG}_<config>_*.
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-TAG=${TAG:-r4}
+TAG=${TAG:-r5}
 B="--steps 1 --warmup 0 --no-cpu-baseline --no-cycle --no-detail-configs --no-transposes"
 F64="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_WAVES"
 for C in ${CONFIGS:-c2 c4 c5}; do
