@@ -501,6 +501,13 @@ def kernel_algorithmic_flops(name, k, solved, nobs_sum):
         return solved * _tri_flops(k, j0, k) + vec
     if name.startswith("solve_tq_kernel") or name.startswith("solve_tq_big_kernel"):
         return syrk + solved * _tri_flops(k, 0, k) + vec
+    # two-stage band path: the head does the O(k^3) part of the reduction (priced as dsytd2's
+    # count, which the band reduction's panels and trailing updates replace); the chase is
+    # O(b k^2) work dsytd2 does not have, so the tail is credited the vector work only
+    if name.startswith("band_head_kernel"):
+        return syrk + solved * _tri_flops(k, 0, k)
+    if name.startswith("band_tail_kernel"):
+        return vec
     if name.startswith("solve_kernel"):  # Jacobi: the eigendecomposition itself
         return synth.flops_total(k, solved, nobs_sum)
     return None

@@ -220,6 +220,14 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
     sm.u.s.u[1][tid] = tid < k ? (double)xbl - xb_mean : 0.0;
   }
 
+  if (CWBL_DBG_STOP(c) == 1) {  // timing ablation: assembly only (keeps the tiles live)
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc += (tile[t][0] + tile[t][1]) + (tile[t][2] + tile[t][3]);
+    rec[HR::BAND + tid] = acc;
+    if (tid == 0) info[gi] = make_int2(ptot, 0);
+    return;
+  }
   // ---- stage 1: 15 panels of 8 columns -------------------------------------------------------
   // the band row i of the record: A(i, i - d), d = 0..8
   auto band_st = [&](int i, int d, double v) { rec[HR::BAND + i * (HR::B + 1) + d] = v; };
@@ -229,7 +237,7 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
     double(*Vb)[8] = sm.u.s.V[p & 1];  // (double buffer: slower waves may still read the last V)
     // (no barrier here: T, Z and M of the previous panel were last read before its barrier B3,
     // and a wave reaches this panel's B1 only after its part of the previous update)
-    if (wave == owner) {
+    if (wave == owner && CWBL_DBG_STOP(c) != 5) {  // (5: timing ablation without the QRs)
       // -- the panel QR, in place in tile column Q, columns 8H .. 8H + 7 -----------------------
       // The QR runs on slot 0's registers: a wave whose panel lies in its second tile column
       // swaps its two slots around it (the tile order of the rest is per slot, so only the QR
@@ -465,6 +473,7 @@ band_head_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab
       }
     }
     __syncthreads();  // B1: V, T of the panel
+    if (CWBL_DBG_STOP(c) == 6) continue;  // timing ablation: the QRs only
 
     // -- W(I) = (A22 V)(I) T for the wave's columns I >= q0 (rows < r0 masked) ------------------
     // V(J) in C/D layout (lane: row 16J + kk + 4r, column m16 < 8) is the B operand of the

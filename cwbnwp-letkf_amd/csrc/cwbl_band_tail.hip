@@ -179,6 +179,10 @@ band_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts, double *__
     }
     __syncthreads();
   }
+  if (CWBL_DBG_STOP(c) == 2) {  // timing ablation: the chase only
+    rec[HR::BAND + l] = band[16 * l] + band[16 * (64 + l)] + sm.b.u[0][l] + sm.b.u[1][l];
+    return;
+  }
   // ---- T: d_i = A(i, i), c(i-1, i) = A(i, i-1) ------------------------------------------------
   double dA = band[16 * l], eA = band[16 * l + 1];
   double dB = band[16 * (64 + l)], eB = band[16 * (64 + l) + 1];
@@ -273,6 +277,10 @@ band_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts, double *__
     }
   }
   __syncthreads();
+  if (CWBL_DBG_STOP(c) == 3) {  // timing ablation: chase + quadrature
+    rec[HR::BAND + l] = sm.b.q.Ym[l] + sm.b.q.Zm[l];
+    return;
+  }
   auto walk = [](int i) { return i < H ? i : H + (KP - 1 - i); };
   const double d = wave_sum_dpp(fma(sm.a.tq[l][2], sm.b.q.Zm[walk(l)],
                                     sm.a.tq[64 + l][2] * sm.b.q.Zm[walk(64 + l)]));
