@@ -392,7 +392,7 @@ def time_config(name, rank, world, local, dev, steps, warmup):
         _, types = cdist.unpack_obs_set(torch.from_numpy(cdist.pack_obs_set(types, w.k)).to(dev))
     x, y, alt, var = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt, w.var))
     del w.var
-    core = abi.Core(w.k, device=local)
+    core = abi.Core(w.k, device=local, options=CORE_OPTIONS)
     core.set_obs(cdist.builder_from(types, abi.MEM_DEVICE).build())
     slab = abi.make_slab(x, y, alt, var, memory=abi.MEM_DEVICE)
     for _ in range(warmup):
@@ -484,6 +484,10 @@ def self_launch(n):
 # A^-1/2 to two vectors through T = Q^T A Q and a quadrature)
 def _tri_flops(k, j0, j1):
     return sum(4 * (k - 1 - j) ** 2 for j in range(j0, min(j1, k - 1)))
+
+
+# cwbl_set_option values for every Core the bench makes (--big-path)
+CORE_OPTIONS = {}
 
 
 def kernel_algorithmic_flops(name, k, solved, nobs_sum):
@@ -634,7 +638,12 @@ def main():
                     help="skip the wall-clock-per-cycle detail (16 var_update entries)")
     ap.add_argument("--no-detail-configs", action="store_true",
                     help="skip the C4 / C5 / host-memory detail legs")
+    ap.add_argument("--big-path", type=int, choices=(0, 1, 2), default=None,
+                    help="CWBL_OPT_BIG_PATH for k > 64 (default: the library's, 1 = hand-off; "
+                         "2 = the two-stage band path at k > 96)")
     args = ap.parse_args()
+    if args.big_path is not None:
+        CORE_OPTIONS["big_path"] = args.big_path
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` without a launcher: start the N ranks ourselves, before
@@ -706,7 +715,7 @@ def run(args, rank, world, stage):
     var = torch.from_numpy(w.var).to(dev)
     torch.cuda.synchronize()
 
-    core = abi.Core(k, device=local)
+    core = abi.Core(k, device=local, options=CORE_OPTIONS)
     core.set_obs(cdist.builder_from(types, abi.MEM_DEVICE).build())
     slab = abi.make_slab(x, y, alt, var, memory=abi.MEM_DEVICE)
 

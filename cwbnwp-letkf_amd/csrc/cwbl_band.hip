@@ -17,12 +17,15 @@
 //     panels' V and T and Q1^T b1, Q1^T x' go to the workspace (BandRec).
 //   band_tail_kernel (one wavefront per point): chases the band to tridiagonal form (1056
 //     Householder reflectors of length <= 8, two sweeps in flight three tasks apart, each task
-//     on 32 lanes: the reflector's left block, diagonal block and the bulge below it as one
-//     instruction stream), the band in LDS (16 KB: row i holds A(i, i-d), d = 0..15);
-//     applies the chase's reflectors to Q1^T b1, Q1^T x' (a sweep's reflectors act on
-//     disjoint rows: 8 at a time), runs the T^-1/2 quadrature of the tail kernel, the
-//     back-transform y <- Q1 Q2 y (chase reflectors sweep by sweep, then the 15 panels) and
-//     the RTPP/RTPS epilogue in the reference's fp32 order.
+//     on 32 lanes: the reflector's left block, diagonal block, the bulge below it and Q2^T on
+//     b1, x' as one instruction stream), the band in LDS (row i holds A(i, i-d), d = 0..15),
+//     then the T^-1/2 quadrature of the tail kernel, the back-transform y <- Q1 Q2 y (chase
+//     reflectors sweep by sweep, then the 15 panels) and the RTPP/RTPS epilogue in the
+//     reference's fp32 order.
+//
+// On gfx950 this path is slower than the hand-off path (the FP64 matrix
+// rate equals the vector rate, so the GEMM form buys no rate while doing twice dsytd2's flops,
+// and the panel QR is a serial chain); it is CWBL_OPT_BIG_PATH = 2, not the default.
 //
 // The design is checked step for step by scripts/two_stage_b8.py (numpy; the same panels,
 // schedule, storage bounds and application orders).  Padding rows (k < 128) are identity rows
