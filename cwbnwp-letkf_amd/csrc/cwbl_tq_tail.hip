@@ -18,11 +18,11 @@
 // A step needs the pivot column per lane and the pivot row as wave-uniform values.  A is
 // kept symmetric (both triangles are updated), so column j is row j: lane j writes its row
 // to LDS once per step (each lane then reads its own entry), and the matvec and the rank-2
-// update take x_c = A(j, c) and w_c straight from lanes j and c (v_readlane).  Row j is
-// never touched again by later steps (v and w vanish there), so after the step it IS the
-// Householder vector (v = scal x, 1 at row j + 1): the back-transform reads it from there.
-// Columns are processed in groups of eight; a group left of the pivot is skipped by a
-// uniform branch, the group holding column j + 1 selects its operands on the scalar unit.
+// update take x_c = A(j, c) and w_c as LDS broadcasts.  Row j is never touched again by
+// later steps (v and w vanish there), so after the step it IS the Householder vector
+// (v = scal x, 1 at row j + 1): the back-transform reads it from there.  Columns are
+// processed in groups of eight; the steps run in blocks by the group of column j + 1, so
+// the groups left of it are skipped at compile time and the rest run without selects.
 #include "cwbl_device.h"
 
 #include <utility>
@@ -51,6 +51,7 @@ template <int KP, int J0>
 struct TailSmem {
   static constexpr int KT = KP - J0;
   double row[KT];         // the pivot row of the step (= its column) / a reflector
+  double wrow[KT];        // w of the step
   double tq[KP + 1][4];   // d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
   double tau[KP];
   double scl[KP];         // this kernel's reflectors: v = scl * x below row j + 1
@@ -136,8 +137,15 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   };
 
   // ---- Householder steps j = J0 .. k-3 (local jl = j - J0) --------------------------------
+  // The steps run in blocks by the group of column j + 1 (gb = (jl + 1) / 8, static): the
+  // groups left of it are skipped at compile time and every other group runs one
+  // branch-free body.  Column j + 1 and the columns left of it in its group need no selects:
+  // once the reflector is formed, the published row gets xt_{j+1} = alpha - beta and zeros
+  // left of it (A(:, c) xt_c and the update then vanish there; w_c = 0 at c <= j as well).
+  // w goes through LDS like the row (two 16-B reads per four columns, no v_readlane).
   const int nst = k - 2 - J0;  // k > J0 + 2 (launcher)
-  for (int jl = 0; jl < nst; ++jl) {
+  auto step = [&](auto GB, int jl) {
+    constexpr int gb = decltype(GB)::value;
     const int j = J0 + jl, j1 = jl + 1;
     publish_row(jl, true);
     const double dj = sm.row[jl], alpha = sm.row[j1];
@@ -166,68 +174,54 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     const double s3 = fma(scal, xb, readlane_f64(u1t, j1));  // v . b1
     u2t = fma(-tau * s2, v, u2t);
     u1t = fma(-tau * s3, v, u1t);
-
     // The uniform side of v: v_c = scal * xt_c with xt_c = x_c = A(j, c) below row j + 1 and
     // xt_{j+1} = alpha - beta = 1/scal (0 when H = I), so column j + 1 needs no special
     // case (v_{j+1} = scal (alpha - beta) is 1 to the last bit or so).
     const double amb = nz ? alpha - bt : 0.0;
-    // A v = scal * sum_{c >= j+1} A(:, c) xt_c; x_c = A(j, c) from the published row (LDS
-    // broadcasts; r4: instead of 16 v_readlane and 8 scalar selects per group), the selects
-    // only in the group of column j + 1; groups left of it are skipped
-    double q[4] = {0.0, 0.0, 0.0, 0.0};  // four chains
-    sfor<NG>([&](auto gg) {
-      constexpr int c0 = 8 * decltype(gg)::value;
-      if (c0 + 7 >= j1) {
-        double xs[8];
-        sfor<4>([&](auto ii) {
-          const double2 x2 = *reinterpret_cast<const double2 *>(&sm.row[c0 + 2 * ii]);
-          xs[2 * ii] = x2.x;
-          xs[2 * ii + 1] = x2.y;
-        });
-        if (c0 > j1) {
-          sfor<8>([&](auto ii) {
-            constexpr int col = c0 + decltype(ii)::value;
-            q[col % 4] = fma(A[col], xs[ii], q[col % 4]);
-          });
-        } else {  // the group of column j + 1
-          sfor<8>([&](auto ii) {
-            constexpr int col = c0 + decltype(ii)::value;
-            const double xt = col > j1 ? xs[ii] : col == j1 ? amb : 0.0;
-            q[col % 4] = fma(A[col], xt, q[col % 4]);
-          });
-        }
-      }
+    __syncthreads();  // every lane has read dj, alpha, its x
+    if (l >= 8 * gb && l <= j1) sm.row[l] = l == j1 ? amb : 0.0;
+    __syncthreads();
+    auto row8 = [&](const double *src, int c0, double (&o)[8]) {
+      sfor<4>([&](auto ii) {
+        const double2 x2 = *reinterpret_cast<const double2 *>(&src[c0 + 2 * ii]);
+        o[2 * ii] = x2.x;
+        o[2 * ii + 1] = x2.y;
+      });
+    };
+    // A v = scal * sum_{c >= j+1} A(:, c) xt_c, four chains
+    double q[4] = {0.0, 0.0, 0.0, 0.0};
+    sfor<NG - gb>([&](auto gg) {
+      constexpr int c0 = 8 * (gb + decltype(gg)::value);
+      double xs[8];
+      row8(sm.row, c0, xs);
+      sfor<8>([&](auto ii) {
+        constexpr int col = c0 + decltype(ii)::value;
+        q[col % 4] = fma(A[col], xs[ii], q[col % 4]);
+      });
     });
     const double av = scal * ((q[0] + q[1]) + (q[2] + q[3]));  // (A v)_l
     const double s1 = tau * wave_sum_dpp(v * av);   // v^T (tau A v); v = 0 at rows <= j
     const double wl = l > jl ? fma(-0.5 * tau * s1, v, tau * av) : 0.0;
     const double wsl = wl * scal;
-    // A <- A - v w^T - w v^T; xt_c from the published row (LDS broadcast), w_c from lane c
-    sfor<NG>([&](auto gg) {
-      constexpr int c0 = 8 * decltype(gg)::value;
-      if (c0 + 7 >= j1) {
-        double wc[8], xs[8];
-        sfor<8>([&](auto ii) { wc[ii] = readlane_f64(wl, c0 + ii); });
-        sfor<4>([&](auto ii) {
-          const double2 x2 = *reinterpret_cast<const double2 *>(&sm.row[c0 + 2 * ii]);
-          xs[2 * ii] = x2.x;
-          xs[2 * ii + 1] = x2.y;
-        });
-        if (c0 > j1) {
-          sfor<8>([&](auto ii) {
-            constexpr int col = c0 + decltype(ii)::value;
-            A[col] = fma(-v, wc[ii], fma(-wsl, xs[ii], A[col]));
-          });
-        } else {  // the group of column j + 1
-          sfor<8>([&](auto ii) {
-            constexpr int col = c0 + decltype(ii)::value;
-            const double xt = col > j1 ? xs[ii] : col == j1 ? amb : 0.0;
-            A[col] = fma(-v, wc[ii], fma(-wsl, xt, A[col]));
-          });
-        }
-      }
+    sm.wrow[l] = wl;
+    __syncthreads();
+    // A <- A - v w^T - w v^T; xt_c and w_c from LDS (broadcast reads)
+    sfor<NG - gb>([&](auto gg) {
+      constexpr int c0 = 8 * (gb + decltype(gg)::value);
+      double wc[8], xs[8];
+      row8(sm.wrow, c0, wc);
+      row8(sm.row, c0, xs);
+      sfor<8>([&](auto ii) {
+        constexpr int col = c0 + decltype(ii)::value;
+        A[col] = fma(-v, wc[ii], fma(-wsl, xs[ii], A[col]));
+      });
     });
-  }
+  };
+  sfor<NG>([&](auto GB) {  // block gb: steps jl = 8 gb - 1 .. 8 gb + 6 (column j + 1 in group gb)
+    constexpr int gb = decltype(GB)::value;
+    const int hi = min(8 * gb + 6, nst - 1);
+    for (int jl = gb == 0 ? 0 : 8 * gb - 1; jl <= hi; ++jl) step(GB, jl);
+  });
   {  // the trailing 2x2 (rows k-2, k-1): already tridiagonal
     const int jl = nst;
     publish_row(jl, false);
