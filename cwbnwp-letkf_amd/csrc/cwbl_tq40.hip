@@ -103,8 +103,9 @@ struct Tq40Smem {
   double tau[4][KP];
 };
 
-// STOP > 0: timing-ablation instantiations (CWBL_DEBUG_TQ_STOP = 4: after the first J0
-// steps, 2: after the tridiagonalisation, 3: after the quadrature; var is not written), so
+// STOP > 0: timing-ablation instantiations (CWBL_DEBUG_TQ_STOP = 5: the record loads only,
+// 4: after the first J0 steps, 2: after the tridiagonalisation, 3: after the quadrature; var
+// is not written), so
 // that the production kernel's code is not perturbed by the early exits
 template <int KP, int STOP = 0>
 __global__ void __launch_bounds__(64, 2)
@@ -201,6 +202,17 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     ux[r] = t < k ? (double)xbl[r + 1] - xb_mean : 0.0;
   });
 
+  if constexpr (STOP == 5) {  // timing ablation: the record loads only (kept live)
+    double acc = uxP + ubP;
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      acc += ux[r] + ub[r];
+      sfor<KP>([&](auto cc) { acc += A[r][decltype(cc)::value]; });
+    });
+    sfor<J0>([&](auto cc) { acc += Pb[decltype(cc)::value]; });
+    if (valid && l == 0) info[gi] = make_int2(ptot, (int)acc);
+    return;
+  }
   // dlarfg with fp64 rcp/rsq refined to ~1 ulp; H = I when x = 0 (tau = 0, v = e_j+1)
   struct Refl {
     double beta, tau, scal;
@@ -697,6 +709,7 @@ hipError_t launch_solve_tq40(hipStream_t s, int kp, SolveConsts c, SlabDev slab,
     case 2: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 2>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
     case 3: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 3>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
     case 4: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 4>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
+    case 5: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 5>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
     default: break;
   }
 #endif

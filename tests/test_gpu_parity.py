@@ -1006,6 +1006,31 @@ def test_pipelined_host_slab_equals_device_slab(tune_q, host, staggered):
     np.testing.assert_array_equal(hv.view(np.uint32), dv.cpu().numpy().view(np.uint32))
 
 
+def test_bounce_slots_after_repeated_init():
+    """The bounce-slot path (option pageable = 1) right after finalize / init, three times:
+    each Core's host worker threads start at the pool's current generation, so no worker runs
+    a stale pass; every result bit-identical to the device-memory call."""
+    torch = pytest.importorskip("torch")
+    _cores.clear()
+    w = _radar_case_scaled(0.1, nz=6)
+    dev = torch.device("cuda:0")
+    x, y, alt, dv = (torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                     for a in (w.x, w.y, w.alt, w.var.copy()))
+    c = abi.Core(w.k, device=0)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    c.analyze_var(w.vp, abi.make_slab(x, y, alt, dv, memory=abi.MEM_DEVICE))
+    c.finalize()
+    want = dv.cpu().numpy().view(np.uint32)
+    for _ in range(3):
+        c = abi.Core(w.k, device=0, options={"max_batch": 2000, "pageable": 1})
+        c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+        hv = w.var.copy()
+        st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, hv))
+        c.finalize()
+        assert st.solved > 0
+        np.testing.assert_array_equal(hv.view(np.uint32), want)
+
+
 def test_set_option_ranges_and_reset():
     """cwbl_set_option: unknown options and out-of-range values are CWBL_ERR_ARG, the Jacobi
     solver past k = 64 is CWBL_ERR_UNSUPPORTED, and cwbl_init resets every option (the
