@@ -222,7 +222,7 @@ struct State {
   DevBuf nbr_cnt2, nbr_idx2;                          // second list buffer (search overlap)
   hipStream_t sstream = nullptr;                      // neighbour searches of later batches
   hipStream_t tstream = nullptr;                      // solve_tq40_kernel (record path)
-  bool tq40_streams = false;  // CWBL_TQ40_STREAMS=1: solve_tq40_kernel on its own stream
+  bool tq40_streams = false;  // CWBL_OPT_SPLIT40_STREAMS: solve_tq40_kernel on its own stream
   DevBuf wsa2, info2;                                 // second record / info buffers
   std::vector<hipEvent_t> cevents;                    // record-path events (cevent)
   int lead_div = 0;                                   // first batch = npts / lead_div (0: off)
@@ -233,22 +233,22 @@ struct State {
   // batches keep each batch's lists and hand-off records nearer the caches and overlap
   // more of the search; below ~70 k the per-batch fixed costs win.
   long long max_batch = 160000;
-  bool max_batch_set = false;                         // CWBL_MAX_BATCH given: no ~6-batch rule
+  bool max_batch_set = false;                         // CWBL_OPT_MAX_BATCH given: no ~6-batch rule
   DevBuf sx, sy, salt, svar;                          // slab staging (host-memory calls)
   DevBuf bcol, byo, byb, bxb, bxa, bev, btri;         // solve_batch staging (btri: T per point)
   DevBuf qxyz, qnf, qidx, qr2;                        // search staging
   DevBuf quad;                                        // x^-1/2 quadrature tables
   DevBuf wsa;                                         // hand-off records (split KP=40 path)
   DevBuf flags;                                       // binned search: flagged points (+ count)
-  bool binned = true;                                 // CWBL_SEARCH=tree: k-d tree search only
-  int bin_div = 0;  // CWBL_BIN_DIV: bin side = radius / bin_div (0: by density, bin_div_for)
-  bool pageable_register = true;                      // CWBL_PAGEABLE=bounce: bounce slots
-  bool jacobi = false;                                // CWBL_SOLVER=jacobi: eigen path
-  int tq4 = 1;  // CWBL_TQ4: KP=40 solve 0 = one kernel, else assembly record + solve_tq40
+  bool binned = true;                                 // CWBL_OPT_SEARCH = 1: k-d tree search only
+  int bin_div = 0;  // CWBL_OPT_BIN_DIV: bin side = radius / bin_div (0: by density, bin_div_for)
+  bool pageable_register = true;                      // CWBL_OPT_PAGEABLE = 1: bounce slots
+  bool jacobi = false;                                // CWBL_OPT_SOLVER = 1: Jacobi eigen path
+  int tq4 = 1;  // CWBL_OPT_SPLIT40: KP=40 solve 0 = one kernel, else assembly record + solve_tq40
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: record batch (points)
   bool big_split = true;                              // big_path 1: hand-off + one-wave tail
   bool band = false;                                  // big_path 2 (KP = 128): two-stage band path
-  long long big_sub = 98304;                          // CWBL_BIG_SUB: KP=128 hand-off batch
+  long long big_sub = 98304;                          // CWBL_OPT_BIG_BATCH: k > 64 sub-batch
   std::vector<hipEvent_t> events;
   hipStream_t h2d = nullptr, d2h = nullptr;           // host-memory slab copies (pipelined)
   hipStream_t caller_stream = nullptr;                // cwbl_set_stream (null: legacy stream)
@@ -474,7 +474,7 @@ hipError_t order_after_caller() {
 // Bin side r / div for the uniform-bin search: r/2 by default; r/4 where the obs are dense
 // (more than 24 per r/2 cell on average over the set's bounding box: the finer cells trim
 // the per-row runs closer to the ball).  r4 A/B: C5 (49 per r/2 cell) 15.95 M pts/s at r/2,
-// 16.04 at r/3, 16.19 at r/4; C2 (~11 per cell) 59.4 / 58.9 / 58.6.  CWBL_BIN_DIV forces it.
+// 16.04 at r/3, 16.19 at r/4; C2 (~11 per cell) 59.4 / 58.9 / 58.6.  CWBL_OPT_BIN_DIV forces it.
 int bin_div_for(const HostTree &t, int dim) {
   if (S.bin_div > 0) return S.bin_div;
   const int n = t.n;
@@ -1026,7 +1026,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   // and then copied like page-locked memory: r4, C2 from pageable numpy arrays 58.7 M pts/s
   // against 58.2 M from page-locked ones and 50.8 M through the bounce slots, whose host
   // copies stall the pipeline.  The slots remain the fallback when the registration fails
-  // (and CWBL_PAGEABLE=bounce forces them).
+  // (and CWBL_OPT_PAGEABLE = 1 forces them).
   bool registered = false;
   if (bounce && S.pageable_register) {
     if (hipHostRegister(sl->var, bvar, hipHostRegisterDefault) == hipSuccess) {
@@ -1547,7 +1547,7 @@ int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const 
   HIPCHK(S.info.ensure((size_t)npts * sizeof(int2)));
   SolveConsts c = solve_consts(inflat, use_rtpp, rtpp_alpha, use_rtps, rtps_alpha);
   // Eigenvalues (dsyevd's ascending eval, module_eigen.f90:48-56): from the tridiagonal T the
-  // tq kernels form, by bisection (launch_tridiag_eigvals), at every k; CWBL_SOLVER=jacobi
+  // tq kernels form, by bisection (launch_tridiag_eigvals), at every k; CWBL_OPT_SOLVER = 1
   // (k <= 64) takes them from the Jacobi eigensolver instead.
   const bool jacobi = S.jacobi && S.kp <= kMaxWaveKP;
   double *tri = nullptr;

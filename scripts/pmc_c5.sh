@@ -2,7 +2,7 @@
 # C5 gather locality: HBM bytes (FETCH_SIZE) and L2 hit rate (TCC_HIT/MISS) per kernel, one
 # step, serial streams -> gpurun_out/pmc_c5/
 cd "$GRAFT_REPO_ROOT"
-export TMPDIR=/tmp CWBL_TQ40_STREAMS=0
+export TMPDIR=/tmp
 OUT=gpurun_out/pmc_c5${TAG:+_$TAG}
 mkdir -p $OUT
 B="python3 bench.py --config ${CFG:-c5} --steps 1 --warmup 0 --no-cpu-baseline --no-cycle --no-detail-configs"

@@ -3,7 +3,7 @@
 profiles/<tag>_summary.json and profiles/pmc_solve_traffic.json (read by bench.py).
 
 HBM bytes per launch of the dominant kernel (solve_tq_kernel, or solve_kernel with
-CWBL_SOLVER=jacobi) follow MI355X_MICROARCH.md
+the Jacobi solver option) follow MI355X_MICROARCH.md
 §HBM: FETCH_SIZE and WRITE_SIZE are in KiB, collected in separate passes; on gfx950
 FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads, so the corrected
 read bytes are 2 x FETCH_SIZE (an upper estimate for this kernel's mixed 4/16-B reads)."""

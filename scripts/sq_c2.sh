@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/sq_${TAG:-r3}
 mkdir -p $OUT
-export CWBL_TQ40_STREAMS=0
+
 B="python3 bench.py --config ${CFG:-c2} --steps 1 --warmup 0 --no-cpu-baseline --no-cycle --no-detail-configs"
 PA="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_VALU_CVT SQ_WAVE_CYCLES"
 PB="SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT"
