@@ -766,7 +766,7 @@ int cwbl_init(const cwbl_init_params *p) {
   S.tq4 = 1;
   S.tq4_sub = 0;
   // r4: one stream by default.  With the r3 kernels the two-stream record path measures a
-  // tie (C2 58.7-59.2 M pts/s either way), and serial launches keep each
+  // tie (C2 58.7-59.2 M pts/s either way, HISTORY.md §3 item 6), and serial launches keep each
   // kernel's duration its own (the per-kernel timing and the roofline read it).
   S.tq40_streams = false;
   S.big_split = true;
@@ -1089,7 +1089,7 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
     for (long long g = g1; g < npts; g += Br)
       plan.push_back({g, (int)std::min<long long>(Br, npts - g)});
     // (a short tail batch, the last batch's final 1/2 or 1/4 split off, measured within the
-    // run-to-run spread at the 8-rank share, r2: DESIGN.md §6)
+    // run-to-run spread at the 8-rank share, r2: HISTORY.md §6)
     B = 0;
     for (const auto &b : plan) B = std::max<long long>(B, b.second);
   }

@@ -138,7 +138,7 @@ def eigen_direct_solve(k, xb, yo, yb, inflat, rp, ra, sp, sa):
     W x' = sqrt(k-1) sum_a q_a (q_a . x') / sqrt(lam_a), never forming Pa = V L^-1 V^T.
     The reference forms Pa (dgemm) and multiplies it by Yb d; when tiny obs errors make
     |Yb d| ~ 1e13 the rounding of Pa's entries alone (~1e-17) moves wbar by ~1e-4 (measured
-    against 60-digit arithmetic: scratch work), whereas here both factors of
+    against 60-digit arithmetic: scratch work, HISTORY.md §4), whereas here both factors of
     the ill-conditioned directions are small.  fp32 inputs and the fp32 epilogue follow the
     reference's order (oracle/letkf_oracle.c:506-541).  yb: (p, k) member fastest."""
     yb8 = np.asarray(yb, np.float64).reshape(-1, k)
