@@ -368,41 +368,37 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     *reinterpret_cast<double2 *>(d) = make_double2(a0, a1);
     *reinterpret_cast<double2 *>(d + 2) = make_double2(a2, a3);
   };
-#define CWBL_PUBLISH(jj, dst)                                                              \
-  do {                                                                                   \
-    const int J_ = (jj) >> 2, q_ = (jj) & 3;                                             \
-    _Pragma("unroll") for (int it = 0; it < NBL; ++it) {                                 \
-      if (tid + NT * it < NBLK && bj[it] == J_) {                                        \
-        double *d_ = &(dst)[4 * bi[it]];                                                 \
-        const double *a_ = acc[it];                                                      \
-        switch (q_) {                                                                    \
-          case 0: pub4(d_, a_[0], a_[4], a_[8], a_[12]); break;                          \
-          case 1: pub4(d_, a_[1], a_[5], a_[9], a_[13]); break;                          \
-          case 2: pub4(d_, a_[2], a_[6], a_[10], a_[14]); break;                         \
-          default: pub4(d_, a_[3], a_[7], a_[11], a_[15]); break;                        \
-        }                                                                                \
-      }                                                                                  \
-    }                                                                                    \
-  } while (0)
+  // (QJ: the column within the block, static: the steps run four to a block column)
+  auto publish = [&](int J_, auto QJ, double *dst) {
+    constexpr int q_ = decltype(QJ)::value;
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) {
+      if (tid + NT * it < NBLK && bj[it] == J_) {
+        const double *a_ = acc[it];
+        pub4(&dst[4 * bi[it]], a_[q_], a_[4 + q_], a_[8 + q_], a_[12 + q_]);
+      }
+    }
+  };
 
   // ---- Householder tridiagonalisation ----------------------------------------------------
   double trace = 0.0;
   static_assert(HS == 0 || (!ASSEMBLED && HS % 4 == 0 && HS + 4 <= KP), "hand-off step");
   // (k > HS + 2 on the split path: every hand-off step is a full step)
   const int jend = HS > 0 ? HS : CWBL_DBG_STEPS(c) > 0 ? min(k, CWBL_DBG_STEPS(c)) : k;
-  for (int j = 0; j < jend; ++j) {
-    const int J = j >> 2, qj = j & 3;
+  auto step = [&](const int j, auto QJ) {
+    constexpr int qj = decltype(QJ)::value;
+    const int J = j >> 2;
     // The previous full step read col only before its four later barriers, so only the
     // step after the (barrier-free) trailing step k-2 needs one here.
     if (j >= k - 1) __syncthreads();
-    CWBL_PUBLISH(j, sm.col);
+    publish(J, QJ, sm.col);
     __syncthreads();
     const double dj = sm.col[j];
     trace += dj;
     if (tid == 0) sm.tq[j][0] = dj;
     if (j >= k - 2) {  // trailing 2x2 block: already tridiagonal
       if (j == k - 2 && tid == 0) sm.tq[j + 1][1] = sm.col[j + 1];
-      continue;
+      return;
     }
     const double x = (tid > j + 1 && tid < k) ? sm.col[tid] : 0.0;
     const double alpha = sm.col[j + 1];
@@ -509,15 +505,16 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[it][4 * r + q] = r >= r0 ? vi[r] : acc[it][4 * r + q];
           };
-          switch (qj) {
-            case 0: keep(std::integral_constant<int, 0>{}); break;
-            case 1: keep(std::integral_constant<int, 1>{}); break;
-            case 2: keep(std::integral_constant<int, 2>{}); break;
-            default: keep(std::integral_constant<int, 3>{}); break;
-          }
+          keep(QJ);
         }
       }
     }
+  };
+  for (int j0 = 0; j0 < jend; j0 += 4) {  // four steps per block column: qj static
+    step(j0, std::integral_constant<int, 0>{});
+    if (j0 + 1 < jend) step(j0 + 1, std::integral_constant<int, 1>{});
+    if (j0 + 2 < jend) step(j0 + 2, std::integral_constant<int, 2>{});
+    if (j0 + 3 < jend) step(j0 + 3, std::integral_constant<int, 3>{});
   }
   if constexpr (HS > 0) {  // hand-off (BigHandoff) after HS steps
     using HO = BigHandoff<KP, HS>;
@@ -777,7 +774,6 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   }
   if (tid == 0 && info) info[gi] = make_int2(ptot, ratio > dec ? -level : level);
 }
-#undef CWBL_PUBLISH
 
 template <int KP>
 static hipError_t launch_big_kp(hipStream_t s, bool assembled, const TreeDesc *trees,
