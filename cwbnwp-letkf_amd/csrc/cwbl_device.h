@@ -7,7 +7,21 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+#include <utility>
+
 namespace cwbl {
+
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>), in order: compile-time
+// blocking of loops whose bodies pick registers or LDS offsets by the index
+template <int... Is, class F>
+__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, Is...>, F &&f) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+  sfor_impl(std::make_integer_sequence<int, N>{}, f);
+}
 
 // ---------------------------------------------------------------------------------------
 // fp32 helpers that must round exactly like the reference build
@@ -124,7 +138,6 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// Sum over each 16-lane row; every lane of a row gets the same (bitwise) row sum.
 // v through a register the compiler cannot see through, after `dep` is known.  The per-row
 // LDS offsets of a quadrature walk whose direction differs per lane (base + dir * t) are
 // loop-invariant: without this the compiler hoists all of them out of the pass loop and holds
@@ -138,6 +151,14 @@ __device__ __forceinline__ double lds_at(const void *base, unsigned off) {
   return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(base) + off);
 }
 
+// v through a register the compiler cannot see through: values formed from it are formed
+// where they are used instead of being hoisted out of the loop around them (and held)
+__device__ __forceinline__ int opaque_int(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// Sum over each 16-lane row; every lane of a row gets the same (bitwise) row sum.
 __device__ __forceinline__ double row16_sum(double v) {
   v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]

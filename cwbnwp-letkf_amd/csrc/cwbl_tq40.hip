@@ -33,15 +33,6 @@ namespace cwbl {
 
 namespace {
 
-template <int... Is, class F>
-__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, Is...>, F &&f) {
-  (f(std::integral_constant<int, Is>{}), ...);
-}
-// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>), in order
-template <int N, class F>
-__device__ __forceinline__ void sfor(F &&f) {
-  sfor_impl(std::make_integer_sequence<int, N>{}, f);
-}
 
 // value of lane L of this lane's 16-lane row (DPP row_newbcast; one v_mov_b64 for fp64,
 // bound_ctrl: every source lane is active)

@@ -21,10 +21,15 @@
 namespace cwbl {
 
 constexpr int kBigThreads = 256;
-// columns staged per chunk: 64 at KP = 128, so that a chunk's MFMA phase (two waves per
-// SIMD) is long enough to cover the next chunk's gathers (stage_columns_pipe)
-template <int KP>
-constexpr int kBigChunk = KP == 128 ? 64 : 32;
+// columns staged per chunk: 64 at KP = 128 on the one-kernel path, so that a chunk's MFMA
+// phase (two waves per SIMD) is long enough to cover the next chunk's gathers
+// (stage_columns_pipe); 32 on the hand-off path, whose LDS then allows three workgroups per CU
+template <int KP, int HS>
+constexpr int kBigChunk = KP == 128 && HS == 0 ? 64 : 32;
+// waves per SIMD the register budget is sized for: the hand-off kernels fit 168 VGPRs (three
+// workgroups per CU); the one-kernel path keeps 256 for the back-transform's registers
+template <int HS>
+constexpr int kBigWaves = HS > 0 ? 3 : 1;
 
 // thread -> 4x4 blocks of the lower block triangle for the tridiagonalisation's benefit.
 // Blocks are numbered column-major over the triangle; block (bi, bj) is read and updated
@@ -63,13 +68,26 @@ __device__ __forceinline__ void big_block_of_lane(int tid, int (&bi)[AsmLayout<K
   }
 }
 
+// last block column of the partial slot NBL - 1 (blocks 0 .. R-1 in column-major order)
 template <int KP>
+constexpr int big_partial_last_column() {
+  using L = AsmLayout<KP, 256>;
+  int b = L::NBLK - 256 * (L::NBL - 1) - 1, cj = 0;
+  while (b >= L::NB - cj) {
+    b -= L::NB - cj;
+    ++cj;
+  }
+  return cj;
+}
+static_assert(big_partial_last_column<128>() == 0 && big_partial_last_column<96>() == 1, "JP");
+
+template <int KP, int CHK>
 struct BigSmem {
   static constexpr int NB = KP / 4;
   static constexpr int PLD = 4 * NB + 4;  // 2*PLD = 8*odd dwords: conflict-free row sums
   union {
     // staged columns (two buffers: stage_columns_pipe); odd columns' rows XOR 16 at KP = 128
-    ColumnChunk<KP, kBigChunk<KP>, float, KP, false, KP == 128> ch[2];
+    ColumnChunk<KP, CHK, float, KP, false, KP == 128> ch[2];
     double pb[NB][PLD];                   // A v partials: pb[R][4c+r] = block (R,c), row r
   } u;
   double col[KP];                         // pivot column / reflector j (back-transform)
@@ -89,7 +107,7 @@ struct BigSmem {
 // HS > 0 (slab path, KP = kBigSplitKP): stop after HS Householder steps and hand the rest
 // over through ws (BigHandoff<KP, HS>) to solve_tqb_tail_kernel.
 template <int KP, bool ASSEMBLED, int HS = 0>
-__global__ void __launch_bounds__(kBigThreads)
+__global__ void __launch_bounds__(kBigThreads, kBigWaves<HS>)
 solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev slab,
                     long long g0, int npts, const int *__restrict__ nbr_cnt,
                     const int *__restrict__ nbr_idx, const long long *__restrict__ col_off,
@@ -100,7 +118,8 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   constexpr int H = KP / 2;
   using L = AsmLayout<KP, NT>;
   constexpr int NBL = L::NBL, NBLK = L::NBLK;
-  using SM = BigSmem<KP>;
+  constexpr int CHK = kBigChunk<KP, HS>;
+  using SM = BigSmem<KP, CHK>;
   static_assert(KP % 8 == 0 && KP <= 2 * 64 && H % 8 == 0, "KP");
   __shared__ SM sm;
 
@@ -229,7 +248,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
       // Yb d (row KP of [Yb; yo] does not fit the tile padding): eight columns per round,
       // their LDS reads issued together, four chains (the staged columns past nsl are zeros)
       if (tid < KP) {
-        constexpr int CH = kBigChunk<KP>;
+        constexpr int CH = CHK;
         const int nr = (nsl + 7) / 8;
         for (int r8 = 0; r8 < nr; ++r8) {
           const float4 o0 = *reinterpret_cast<const float4 *>(&cb.yo[8 * r8]);
@@ -245,10 +264,10 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
       }
     };
     if constexpr (!ASSEMBLED)
-      ptot = stage_columns_pipe<KP, kBigChunk<KP>, NT>(sm.u.ch, trees, c, gi, tid, nbr_cnt, nbr_idx,
+      ptot = stage_columns_pipe<KP, CHK, NT>(sm.u.ch, trees, c, gi, tid, nbr_cnt, nbr_idx,
                                                    pt, mfma_chunk);
     else
-      ptot = stage_columns<KP, kBigChunk<KP>, ASSEMBLED, NT>(
+      ptot = stage_columns<KP, CHK, ASSEMBLED, NT>(
           sm.u.ch[0], trees, c, gi, tid, nbr_cnt, nbr_idx, pt, col_off, yo_in, yb_in,
           [&](int nsl) { mfma_chunk(nsl, sm.u.ch[0]); });
     b1acc = (b1p[0] + b1p[1]) + (b1p[2] + b1p[3]);
@@ -261,9 +280,8 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
       const int wI = I <= 3 ? I : 7 - I, t = I <= 3 ? J : 8 - I + J;
       rnd[it] = t >> 2;
       off[it] = (4 * wI + (t & 3)) * 256 + (4 * (bi[it] & 3)) * 16 + 4 * (bj[it] & 3);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[it][e] = 0.0;
-    }
+    }  // (no zero fill: a slot is read only where tid + NT it < NBLK, and a fill would keep all
+       // of acc live beside the tiles)
     double *tl = &sm.u.pb[0][0];
 #pragma unroll
     for (int rd = 0; rd < 3; ++rd) {
@@ -293,7 +311,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
       }
     }
   } else {
-    assemble_point<KP, kBigChunk<KP>, ASSEMBLED, NT>(sm.u.ch[0], trees, c, gi, tid, nbr_cnt, nbr_idx,
+    assemble_point<KP, CHK, ASSEMBLED, NT>(sm.u.ch[0], trees, c, gi, tid, nbr_cnt, nbr_idx,
                                                  pt, col_off, yo_in, yb_in, bi, bj, acc, b1acc,
                                                  ptot);
   }
@@ -315,7 +333,8 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   if (CWBL_DBG_STOP(c) == 1 || CWBL_DBG_STOP(c) == 12) {  // timing ablation: assembly only
     double t = b1acc;
 #pragma unroll
-    for (int it = 0; it < NBL; ++it) t += acc[it][0] + acc[it][15];
+    for (int it = 0; it < NBL; ++it)
+      if (tid + NT * it < NBLK) t += acc[it][0] + acc[it][15];
     if (tid == 0 && info) info[gi] = make_int2(ptot, (int)t);
     return;
   }
@@ -369,13 +388,14 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     *reinterpret_cast<double2 *>(d + 2) = make_double2(a2, a3);
   };
   // (QJ: the column within the block, static: the steps run four to a block column)
-  auto publish = [&](int J_, auto QJ, double *dst) {
+  auto publish = [&](int J_, auto QJ, auto NS, const int (&bI)[NBL], const int (&bJ)[NBL],
+                     double *dst) {
     constexpr int q_ = decltype(QJ)::value;
 #pragma unroll
-    for (int it = 0; it < NBL; ++it) {
-      if (tid + NT * it < NBLK && bj[it] == J_) {
+    for (int it = 0; it < decltype(NS)::value; ++it) {
+      if (tid + NT * it < NBLK && bJ[it] == J_) {
         const double *a_ = acc[it];
-        pub4(&dst[4 * bi[it]], a_[q_], a_[4 + q_], a_[8 + q_], a_[12 + q_]);
+        pub4(&dst[4 * bI[it]], a_[q_], a_[4 + q_], a_[8 + q_], a_[12 + q_]);
       }
     }
   };
@@ -385,13 +405,23 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   static_assert(HS == 0 || (!ASSEMBLED && HS % 4 == 0 && HS + 4 <= KP), "hand-off step");
   // (k > HS + 2 on the split path: every hand-off step is a full step)
   const int jend = HS > 0 ? HS : CWBL_DBG_STEPS(c) > 0 ? min(k, CWBL_DBG_STEPS(c)) : k;
-  auto step = [&](const int j, auto QJ) {
-    constexpr int qj = decltype(QJ)::value;
+  // NS: the slots a step visits (static).  The partial slot NBL - 1 holds only blocks of block
+  // columns <= JP, so the steps past block column JP leave it out and its registers are free
+  auto step = [&](const int j, auto QJ, auto NS) {
+    constexpr int ns = decltype(NS)::value;
+    // the slots' block indices through opaque registers: the LDS addresses formed from them
+    // live for one step, not for the whole loop (hoisted, they did not fit 168 VGPRs)
+    int bI[NBL], bJ[NBL];
+#pragma unroll
+    for (int it = 0; it < NBL; ++it) {
+      bI[it] = opaque_int(bi[it]);
+      bJ[it] = opaque_int(bj[it]);
+    }
     const int J = j >> 2;
     // The previous full step read col only before its four later barriers, so only the
     // step after the (barrier-free) trailing step k-2 needs one here.
     if (j >= k - 1) __syncthreads();
-    publish(J, QJ, sm.col);
+    publish(J, QJ, NS, bI, bJ, sm.col);
     __syncthreads();
     const double dj = sm.col[j];
     trace += dj;
@@ -429,11 +459,11 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     __syncthreads();
     double s1p = 0.0;
 #pragma unroll
-    for (int it = 0; it < NBL; ++it) {
-      if (tid + NT * it < NBLK && bj[it] >= J) {
+    for (int it = 0; it < ns; ++it) {
+      if (tid + NT * it < NBLK && bJ[it] >= J) {
         double vi[4], vj[4];
-        ld4s(&sm.vb[4 * bi[it]], hsw(bi[it]), vi);
-        ld4s(&sm.vb[4 * bj[it]], hsw(bj[it]), vj);
+        ld4s(&sm.vb[4 * bI[it]], hsw(bI[it]), vi);
+        ld4s(&sm.vb[4 * bJ[it]], hsw(bJ[it]), vj);
         double pr[4], pc[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -450,10 +480,10 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
         double sp = vi[0] * pr[0];
 #pragma unroll
         for (int r = 1; r < 4; ++r) sp = fma(vi[r], pr[r], sp);
-        st4s(&sm.u.pb[bi[it]][4 * bj[it]], hsw(bi[it]), pr[0], pr[1], pr[2], pr[3]);
-        if (bi[it] != bj[it]) {
-          if (bj[it] >= J)
-            st4s(&sm.u.pb[bj[it]][4 * bi[it]], hsw(bj[it]), pc[0], pc[1], pc[2], pc[3]);
+        st4s(&sm.u.pb[bI[it]][4 * bJ[it]], hsw(bI[it]), pr[0], pr[1], pr[2], pr[3]);
+        if (bI[it] != bJ[it]) {
+          if (bJ[it] >= J)
+            st4s(&sm.u.pb[bJ[it]][4 * bI[it]], hsw(bJ[it]), pc[0], pc[1], pc[2], pc[3]);
           sp = sp + sp;
         }
         s1p += sp;
@@ -486,20 +516,20 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     if (tid < KP) sm.wb[tsw] = w;
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < NBL; ++it) {
-      if (tid + NT * it < NBLK && bj[it] >= J) {
+    for (int it = 0; it < ns; ++it) {
+      if (tid + NT * it < NBLK && bJ[it] >= J) {
         double vi[4], vj[4], wi[4], wj[4];
-        ld4s(&sm.vb[4 * bi[it]], hsw(bi[it]), vi);
-        ld4s(&sm.vb[4 * bj[it]], hsw(bj[it]), vj);
-        ld4s(&sm.wb[4 * bi[it]], hsw(bi[it]), wi);
-        ld4s(&sm.wb[4 * bj[it]], hsw(bj[it]), wj);
+        ld4s(&sm.vb[4 * bI[it]], hsw(bI[it]), vi);
+        ld4s(&sm.vb[4 * bJ[it]], hsw(bJ[it]), vj);
+        ld4s(&sm.wb[4 * bI[it]], hsw(bI[it]), wi);
+        ld4s(&sm.wb[4 * bJ[it]], hsw(bJ[it]), wj);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             acc[it][4 * r + q] = fma(-vi[r], wj[q], fma(-wi[r], vj[q], acc[it][4 * r + q]));
-        if (bj[it] == J) {  // keep v_j in the entries of column j the steps no longer read
-          const int r0 = j + 2 - 4 * bi[it];  // rows r >= r0 of the block
+        if (bJ[it] == J) {  // keep v_j in the entries of column j the steps no longer read
+          const int r0 = j + 2 - 4 * bI[it];  // rows r >= r0 of the block
           auto keep = [&](auto Q) {
             constexpr int q = decltype(Q)::value;
 #pragma unroll
@@ -510,19 +540,20 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
       }
     }
   };
-  for (int j0 = 0; j0 < jend; j0 += 4) {  // four steps per block column: qj static
-    step(j0, std::integral_constant<int, 0>{});
-    if (j0 + 1 < jend) step(j0 + 1, std::integral_constant<int, 1>{});
-    if (j0 + 2 < jend) step(j0 + 2, std::integral_constant<int, 2>{});
-    if (j0 + 3 < jend) step(j0 + 3, std::integral_constant<int, 3>{});
-  }
-  if constexpr (HS > 0) {  // hand-off (BigHandoff) after HS steps
-    using HO = BigHandoff<KP, HS>;
+  auto block_column = [&](int j0, auto NS) {  // four steps per block column: qj static
+    step(j0, std::integral_constant<int, 0>{}, NS);
+    if (j0 + 1 < jend) step(j0 + 1, std::integral_constant<int, 1>{}, NS);
+    if (j0 + 2 < jend) step(j0 + 2, std::integral_constant<int, 2>{}, NS);
+    if (j0 + 3 < jend) step(j0 + 3, std::integral_constant<int, 3>{}, NS);
+  };
+  // hand-off (BigHandoff) of slot it's blocks: trailing blocks as the full matrix, the others
+  // as reflector columns
+  auto handoff_slot = [&](auto IT) {
+    constexpr int it = decltype(IT)::value;
+    using HO = BigHandoff<KP, (HS > 0 ? HS : 4)>;
     constexpr int KT = HO::KT, JB = HS / 4;
     double *__restrict__ w = ws + (long long)gi * HO::WORDS;
-    __syncthreads();  // T, tau of the last steps are in LDS
-#pragma unroll
-    for (int it = 0; it < NBL; ++it) {
+    {
       if (tid + NT * it < NBLK) {
         if (bj[it] >= JB) {  // trailing block: both triangles of the full KT x KT matrix
           const int a0 = 4 * (bi[it] - JB), b0 = 4 * (bj[it] - JB);
@@ -553,6 +584,20 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
         }
       }
     }
+  };
+  constexpr int JP = big_partial_last_column<KP>();
+  int j0 = 0;
+  for (; j0 < jend && j0 < 4 * (JP + 1); j0 += 4) block_column(j0, std::integral_constant<int, NBL>{});
+  // on the hand-off path the partial slot's blocks (reflector columns <= JP) go out now, so that
+  // its registers are free for the remaining steps
+  if constexpr (HS > 0) handoff_slot(std::integral_constant<int, NBL - 1>{});
+  for (; j0 < jend; j0 += 4) block_column(j0, std::integral_constant<int, NBL - 1>{});
+  if constexpr (HS > 0) {  // hand-off (BigHandoff) after HS steps
+    using HO = BigHandoff<KP, HS>;
+    static_assert(JP < HS / 4, "the partial slot holds reflector columns only");
+    double *__restrict__ w = ws + (long long)gi * HO::WORDS;
+    __syncthreads();  // T, tau of the last steps are in LDS
+    sfor<NBL - 1>([&](auto IT) { handoff_slot(IT); });
     if (tid < KP) {
       w[HO::U1 + tid] = ub;
       w[HO::U2 + tid] = ux;

@@ -31,15 +31,6 @@ namespace cwbl {
 
 namespace {
 
-template <int... Is, class F>
-__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, Is...>, F &&f) {
-  (f(std::integral_constant<int, Is>{}), ...);
-}
-// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>), in order
-template <int N, class F>
-__device__ __forceinline__ void sfor(F &&f) {
-  sfor_impl(std::make_integer_sequence<int, N>{}, f);
-}
 
 __device__ __forceinline__ float readlane_f32(float x, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l));
