@@ -138,6 +138,64 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// ---- 16-lane row broadcasts (gfx950's 64-bit DPP is row_newbcast only) ------------------
+// value of lane L of this lane's 16-lane row (one v_mov_b64 DPP; bound_ctrl: every source
+// lane is active)
+template <int L>
+__device__ __forceinline__ double rbcast(double x) {
+  return __longlong_as_double(
+      __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x150 + L, 0xf, 0xf, true));
+}
+template <int L>
+__device__ __forceinline__ float rbcast(float x) {
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x150 + L, 0xf, 0xf, true));
+}
+// acc + x_L y and acc - x_L y, x_L = lane L of this lane's 16-lane row: one v_fmac_f64_dpp
+// row_newbcast instead of a v_mov_b64_dpp broadcast and an FMA.  The compiler does not form
+// it itself (its DPP combine sees the three-address v_fma_f64).  A DPP source must not be
+// written by the VALU in the two instructions before: callers write their sources once and
+// pin them behind an s_nop 1 (dpp_pin) before the first use; the compiler's hazard check
+// covers the inline asm's other operands.
+template <int L>
+__device__ __forceinline__ double fmac_row(double acc, double x, double y) {
+  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "+v"(acc) : "v"(x), "v"(y), "i"(L));
+  return acc;
+}
+template <int L>
+__device__ __forceinline__ double fnmac_row(double acc, double x, double y) {
+  asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "+v"(acc) : "v"(x), "v"(y), "i"(L));
+  return acc;
+}
+__device__ __forceinline__ void dpp_pin(double &x) { asm volatile("s_nop 1" : "+v"(x)); }
+// the same as volatile statements: kept in program order relative to each other and to the
+// volatile s_nop that opens a pass (dpp_fence), so no VALU write of a DPP source lands within
+// two instructions of its read
+template <int L>
+__device__ __forceinline__ double fmac_row_v(double acc, double x, double y) {
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+               : "+v"(acc) : "v"(x), "v"(y), "i"(L));
+  return acc;
+}
+template <int L>
+__device__ __forceinline__ double fnmac_row_v(double acc, double x, double y) {
+  asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+               : "+v"(acc) : "v"(x), "v"(y), "i"(L));
+  return acc;
+}
+__device__ __forceinline__ void dpp_fence() { asm volatile("s_nop 1" ::: "memory"); }
+// value of lane l ^ 8 of the row (row_ror:8)
+__device__ __forceinline__ double ror8(double x) { return dpp_f64<0x128>(x); }
+// sum over each 8-lane half of a 16-lane row (quad sums, then the half mirror)
+__device__ __forceinline__ double rsum8(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  return v;
+}
+
 // v through a register the compiler cannot see through, after `dep` is known.  The per-row
 // LDS offsets of a quadrature walk whose direction differs per lane (base + dir * t) are
 // loop-invariant: without this the compiler hoists all of them out of the pass loop and holds

@@ -34,41 +34,6 @@ namespace cwbl {
 namespace {
 
 
-// value of lane L of this lane's 16-lane row (DPP row_newbcast; one v_mov_b64 for fp64,
-// bound_ctrl: every source lane is active)
-template <int L>
-__device__ __forceinline__ double rbcast(double x) {
-  return __longlong_as_double(
-      __builtin_amdgcn_update_dpp(0ll, __double_as_longlong(x), 0x150 + L, 0xf, 0xf, true));
-}
-template <int L>
-__device__ __forceinline__ float rbcast(float x) {
-  return __int_as_float(
-      __builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x150 + L, 0xf, 0xf, true));
-}
-// value of lane l ^ 8 of the row (row_ror:8)
-__device__ __forceinline__ double ror8(double x) { return dpp_f64<0x128>(x); }
-
-// acc + x_L y and acc - x_L y, x_L = lane L of this lane's 16-lane row: one v_fmac_f64_dpp
-// row_newbcast (gfx950's 64-bit DPP) instead of a v_mov_b64_dpp broadcast and an FMA.  The
-// compiler does not form it itself (its DPP combine sees the three-address v_fma_f64).  A
-// DPP source must not be written by the VALU in the two instructions before; the steps write
-// their sources once and pin them behind an s_nop 1 (dpp_pin) before the first use, and the
-// compiler's hazard check covers the inline asm's other operands.
-template <int L>
-__device__ __forceinline__ double fmac_row(double acc, double x, double y) {
-  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-      : "+v"(acc) : "v"(x), "v"(y), "i"(L));
-  return acc;
-}
-template <int L>
-__device__ __forceinline__ double fnmac_row(double acc, double x, double y) {
-  asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-      : "+v"(acc) : "v"(x), "v"(y), "i"(L));
-  return acc;
-}
-__device__ __forceinline__ void dpp_pin(double &x) { asm volatile("s_nop 1" : "+v"(x)); }
-
 // Sum over this lane's 16-lane row, the same value on every lane: two quad_perm stages (two
 // v_mov_b32_dpp and a v_add_f64 each: gfx950 has no 64-bit quad_perm), then the four quad
 // sums Q0 + Q4 + Q8 + Q12 as one row_newbcast move and three fused v_fmac_f64_dpp (x 1.0,

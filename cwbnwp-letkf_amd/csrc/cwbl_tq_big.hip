@@ -98,7 +98,6 @@ struct BigSmem {
   double tau[KP];
   double red[2][4][4];                    // [buffer][wave][value] of the block reductions
   double red10[4][10];                    // [wave][value]: back-transform group reduction
-  double piv[2];                          // x'_{j+1}, b1_{j+1} of the current step
   double pard;                            // sequential-sum partial handed wave to wave
   float parf;
   int ptot;
@@ -142,15 +141,6 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     b = (r[0][1] + r[1][1]) + (r[2][1] + r[3][1]);
     cc = (r[0][2] + r[1][2]) + (r[2][2] + r[3][2]);
     d = (r[0][3] + r[1][3]) + (r[2][3] + r[3][3]);
-  };
-  // one value: wave sum + the 4-entry exchange (buffers shared with bsum4's rotation)
-  auto bsum1 = [&](double a) {
-    a = wave_sum_dpp(a);
-    double(*r)[4] = sm.red[rbuf];
-    rbuf ^= 1;
-    if (lane == 0) r[wave][0] = a;
-    __syncthreads();
-    return (r[0][0] + r[1][0]) + (r[2][0] + r[3][0]);
   };
   // the reference's sequential member-order sums (member m lives in thread m), wave by wave
   auto seq_sum_f32 = [&](float x) {
@@ -404,7 +394,9 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
   double trace = 0.0;
   static_assert(HS == 0 || (!ASSEMBLED && HS % 4 == 0 && HS + 4 <= KP), "hand-off step");
   // (k > HS + 2 on the split path: every hand-off step is a full step)
-  const int jend = HS > 0 ? HS : CWBL_DBG_STEPS(c) > 0 ? min(k, CWBL_DBG_STEPS(c)) : k;
+  // (debug_steps: timing ablation, the first steps only; the hand-off then carries a partial
+  // reduction)
+  const int jend = CWBL_DBG_STEPS(c) > 0 ? min(HS > 0 ? HS : k, CWBL_DBG_STEPS(c)) : HS > 0 ? HS : k;
   // NS: the slots a step visits (static).  The partial slot NBL - 1 holds only blocks of block
   // columns <= JP, so the steps past block column JP leave it out and its registers are free
   auto step = [&](const int j, auto QJ, auto NS) {
@@ -417,12 +409,34 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
       bI[it] = opaque_int(bi[it]);
       bJ[it] = opaque_int(bj[it]);
     }
+    constexpr int qj = decltype(QJ)::value;
     const int J = j >> 2;
-    // The previous full step read col only before its four later barriers, so only the
+    // The previous full step read col only before its three later barriers, so only the
     // step after the (barrier-free) trailing step k-2 needs one here.
     if (j >= k - 1) __syncthreads();
     publish(J, QJ, NS, bI, bJ, sm.col);
+    // x.x (x = column j below row j + 1) from the owners' registers, reduced with the publish
+    // barrier.  Rows >= k hold exact zeros in columns < k, so no row bound is needed.
+    {
+      double xs = 0.0;
+#pragma unroll
+      for (int it = 0; it < ns; ++it) {
+        if (tid + NT * it < NBLK && bJ[it] == J) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {  // row 4 bI + r > j + 1
+            const bool below = bI[it] > J + 1 || (bI[it] == J ? r > qj + 1 : r > qj - 3);
+            const double a = acc[it][4 * r + qj];
+            xs = below ? fma(a, a, xs) : xs;
+          }
+        }
+      }
+      xs = wave_sum_dpp(xs);
+      if (lane == 0) sm.red[rbuf][wave][0] = xs;
+    }
     __syncthreads();
+    const double xn2 = (sm.red[rbuf][0][0] + sm.red[rbuf][1][0]) +
+                       (sm.red[rbuf][2][0] + sm.red[rbuf][3][0]);
+    rbuf ^= 1;
     const double dj = sm.col[j];
     trace += dj;
     if (tid == 0) sm.tq[j][0] = dj;
@@ -432,9 +446,6 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     }
     const double x = (tid > j + 1 && tid < k) ? sm.col[tid] : 0.0;
     const double alpha = sm.col[j + 1];
-    // x.x, x.x', x.b1 in one reduction: v = x scal + e_{j+1}, so v.u = scal (x.u) + u_{j+1}
-    double xn2 = x * x, xux = x * ux, xub = x * ub, z3 = 0.0;
-    bsum4(xn2, xux, xub, z3);
     double tau = 0.0, beta = alpha, scal = 0.0;
     if (xn2 > 0.0) {  // dlarfg, fp64 rcp/rsq refined to ~1 ulp
       const double a2 = fma(alpha, alpha, xn2);
@@ -452,10 +463,6 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     // (j = 4 bj + 3, where v vanishes on its columns) leaving exact zeros in its A v partials.
     const double v = tid == j + 1 ? 1.0 : x * scal;
     if (tid < KP) sm.vb[tsw] = v;
-    if (tid == j + 1) {  // x'_{j+1}, b1_{j+1} for every thread's v.x', v.b1
-      sm.piv[0] = ux;
-      sm.piv[1] = ub;
-    }
     __syncthreads();
     double s1p = 0.0;
 #pragma unroll
@@ -489,11 +496,12 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
         s1p += sp;
       }
     }
-    const double s2 = fma(scal, xux, sm.piv[0]), s3 = fma(scal, xub, sm.piv[1]);
+    // v.A v, v.x', v.b1 in one reduction (its barrier also publishes pb)
+    double s2 = v * ux, s3 = v * ub, z3 = 0.0;
+    bsum4(s1p, s2, s3, z3);
     ux = fma(-tau * s2, v, ux);
     ub = fma(-tau * s3, v, ub);
-    double s1 = bsum1(s1p);  // also publishes pb (barrier inside)
-    s1 *= tau;               // p . v with p = tau A v
+    const double s1 = s1p * tau;  // p . v with p = tau A v
     double pp = 0.0;
     if (tid < KP && tid > j) {
       const double *prow = &sm.u.pb[tid >> 2][tsw & 3];

@@ -5,7 +5,7 @@
 // solve_tq_big_kernel<KP, false, J0> (cwbl_tq_big.hip) stages the point's columns, assembles
 // A = (k-1)/infl I + Yb Yb^T and b1 = Yb d on the matrix cores and runs the first J0 steps of
 // the Householder tridiagonalisation A = Q T Q^T (dsytd2 order) on 4x4 register blocks spread
-// over a 256-thread workgroup; each of its steps is a chain of five barriers and LDS
+// over a 256-thread workgroup; each of its steps is a chain of four barriers and LDS
 // exchanges, so its cost per step is nearly fixed.  It hands the trailing KT x KT matrix,
 // its J0 reflectors, T so far and Q^T b1, Q^T x' over through the workspace (BigHandoff).
 // This kernel finishes the algorithm — the remaining steps, the T^-1/2 quadrature and the
@@ -15,14 +15,16 @@
 //   lane l holds the FULL trailing row J0 + l (KT = 64 doubles, static register indices)
 //   and the vectors' rows l (prefix) and J0 + l (trailing).
 //
-// A step needs the pivot column per lane and the pivot row as wave-uniform values.  A is
-// kept symmetric (both triangles are updated), so column j is row j: lane j writes its row
-// to LDS once per step (each lane then reads its own entry), and the matvec and the rank-2
-// update take x_c = A(j, c) and w_c as LDS broadcasts.  Row j is never touched again by
-// later steps (v and w vanish there), so after the step it IS the Householder vector
-// (v = scal x, 1 at row j + 1): the back-transform reads it from there.  Columns are
-// processed in groups of eight; the steps run in blocks by the group of column j + 1, so
-// the groups left of it are skipped at compile time and the rest run without selects.
+// A step needs the pivot column per lane and the pivot row's entries as operands of every
+// lane.  A is kept symmetric (both triangles are updated), so lane l's entry A(l, j) is the
+// pivot row's entry l: each lane picks it from its registers, two v_permlane swaps per half
+// copy the row into four row-replicated registers, and the matvec and the rank-2 update take
+// x_c = A(j, c) and w_c as the row_newbcast operand of a fused v_fmac_f64_dpp — no LDS in the
+// step.  Row j is never touched again by later steps (v and w vanish there), so it IS the
+// Householder vector (v = scal x, 1 at row j + 1): each lane parks its entry in the record's
+// scratch rows, where the back-transform reads it.  Columns are processed in groups of
+// eight; the steps run in blocks by the group of column j + 1, so the groups left of it are
+// skipped at compile time and the rest run without selects.
 #include "cwbl_device.h"
 
 #include <utility>
@@ -41,8 +43,7 @@ __device__ __forceinline__ float readlane_f32(float x, int l) {
 template <int KP, int J0>
 struct TailSmem {
   static constexpr int KT = KP - J0;
-  double row[KT];         // the pivot row of the step (= its column) / a reflector
-  double wrow[KT];        // w of the step
+  double row[KT];         // a row of the trailing 2x2 block's step
   double tq[KP + 1][4];   // d_i, c(i-1,i), (Q^T b1)_i, (Q^T x')_i
   double tau[KP];
   double scl[KP];         // this kernel's reflectors: v = scl * x below row j + 1
@@ -111,36 +112,69 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   double trace = 0.0;  // d_0 + d_1 + ... in step order, as solve_tq_big_kernel sums it
   for (int j = 0; j < J0; ++j) trace += sm.tq[j][0];
 
-  // lane jl's row -> sm.row (static register indices); with `park`, also to the record's
-  // scratch rows (BT), where the back-transform finds it once the registers are released
-  double *__restrict__ parked = ws + (long long)gi * HO::WORDS + HO::BT;
-  auto publish_row = [&](int jl, bool park) {
+  // lane jl's row -> sm.row (static register indices): the trailing 2x2 block's entries
+  auto publish_row = [&](int jl) {
     __syncthreads();  // the previous readers of sm.row are done
     if (l == jl) {
       sfor<KT / 2>([&](auto cc) {
         constexpr int col = 2 * decltype(cc)::value;
-        const double2 p2 = make_double2(A[col], A[col + 1]);
-        *reinterpret_cast<double2 *>(&sm.row[col]) = p2;
-        if (park) *reinterpret_cast<double2 *>(&parked[jl * KT + col]) = p2;
+        *reinterpret_cast<double2 *>(&sm.row[col]) = make_double2(A[col], A[col + 1]);
       });
     }
     __syncthreads();
   };
+  // the record's scratch rows (BT): row jl of this kernel's steps, where the back-transform
+  // finds it once the registers are released
+  double *__restrict__ parked = ws + (long long)gi * HO::WORDS + HO::BT;
 
   // ---- Householder steps j = J0 .. k-3 (local jl = j - J0) --------------------------------
-  // The steps run in blocks by the group of column j + 1 (gb = (jl + 1) / 8, static): the
-  // groups left of it are skipped at compile time and every other group runs one
-  // branch-free body.  Column j + 1 and the columns left of it in its group need no selects:
-  // once the reflector is formed, the published row gets xt_{j+1} = alpha - beta and zeros
-  // left of it (A(:, c) xt_c and the update then vanish there; w_c = 0 at c <= j as well).
-  // w goes through LDS like the row (two 16-B reads per four columns, no v_readlane).
+  // A is symmetric, so lane l's entry A[jl] is the pivot row's entry l.  The pivot row and w
+  // reach the lanes without LDS: rep4 copies them into four row-replicated registers (every
+  // 16-lane row of R[g] holds entries 16g .. 16g+15) and the matvec and the rank-2 update take
+  // entry c as the row_newbcast operand of a fused v_fmac_f64_dpp.  The steps run in blocks by
+  // the group of column j + 1 (gb = (jl + 1) / 8, static): the 8-column groups left of it are
+  // skipped at compile time, and the pivot column is picked from the block's eight registers
+  // by value.  Column j + 1 and the columns left of it in its group need no selects: the
+  // replicated row carries xt_{j+1} = alpha - beta and zeros left of it (A(:, c) xt_c and the
+  // update then vanish there; w_c = 0 at c <= j as well).
+  auto rep4 = [](double x, double (&R)[4]) {
+    const int xl = (int)__double_as_longlong(x), xh = (int)(__double_as_longlong(x) >> 32);
+    auto mk = [](int lo, int hi) {
+      return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+    };
+    // rows (0, 1, 0, 1) and (2, 3, 2, 3), then each row of those over its pair
+    const auto al = __builtin_amdgcn_permlane32_swap(xl, xl, false, false);
+    const auto ah = __builtin_amdgcn_permlane32_swap(xh, xh, false, false);
+    const auto bl = __builtin_amdgcn_permlane16_swap(al[0], al[0], false, false);
+    const auto bh = __builtin_amdgcn_permlane16_swap(ah[0], ah[0], false, false);
+    const auto cl = __builtin_amdgcn_permlane16_swap(al[1], al[1], false, false);
+    const auto ch = __builtin_amdgcn_permlane16_swap(ah[1], ah[1], false, false);
+    R[0] = mk(bl[0], bh[0]);
+    R[1] = mk(bl[1], bh[1]);
+    R[2] = mk(cl[0], ch[0]);
+    R[3] = mk(cl[1], ch[1]);
+    // a DPP source is not read within two wait states of its VALU write
+    asm volatile("s_nop 1" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]));
+  };
   const int nst = k - 2 - J0;  // k > J0 + 2 (launcher)
   auto step = [&](auto GB, int jl) {
     constexpr int gb = decltype(GB)::value;
+    constexpr int jb = gb == 0 ? 0 : 8 * gb - 1;  // the block's first step
     const int j = J0 + jl, j1 = jl + 1;
-    publish_row(jl, true);
-    const double dj = sm.row[jl], alpha = sm.row[j1];
-    const double xr = sm.row[l];  // A(J0 + l, j)
+    // A(J0 + l, j) = A[jl], picked by value: the candidates pass an empty asm, so that the
+    // compiler cannot fold the selects of register-array loads into one load through a
+    // selected address (which sends all of A to scratch memory)
+    auto opq = [](double a) {
+      asm("" : "+v"(a));
+      return a;
+    };
+    double xr = opq(A[jb]);
+    sfor<7>([&](auto ii) {
+      constexpr int cc = jb + 1 + decltype(ii)::value;
+      if constexpr (cc < KT) xr = jl == cc ? opq(A[cc]) : xr;
+    });
+    parked[jl * KT + l] = xr;
+    const double dj = readlane_f64(xr, jl), alpha = readlane_f64(xr, j1);
     trace += dj;
     const double x = l > j1 ? xr : 0.0;
     double xx = x * x, xu = x * u2t, xb = x * u1t, z3 = 0.0;
@@ -169,42 +203,32 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     // xt_{j+1} = alpha - beta = 1/scal (0 when H = I), so column j + 1 needs no special
     // case (v_{j+1} = scal (alpha - beta) is 1 to the last bit or so).
     const double amb = nz ? alpha - bt : 0.0;
-    __syncthreads();  // every lane has read dj, alpha, its x
-    if (l >= 8 * gb && l <= j1) sm.row[l] = l == j1 ? amb : 0.0;
-    __syncthreads();
-    auto row8 = [&](const double *src, int c0, double (&o)[8]) {
-      sfor<4>([&](auto ii) {
-        const double2 x2 = *reinterpret_cast<const double2 *>(&src[c0 + 2 * ii]);
-        o[2 * ii] = x2.x;
-        o[2 * ii + 1] = x2.y;
-      });
-    };
-    // A v = scal * sum_{c >= j+1} A(:, c) xt_c, four chains
-    double q[4] = {0.0, 0.0, 0.0, 0.0};
-    sfor<NG - gb>([&](auto gg) {
-      constexpr int c0 = 8 * (gb + decltype(gg)::value);
-      double xs[8];
-      row8(sm.row, c0, xs);
-      sfor<8>([&](auto ii) {
-        constexpr int col = c0 + decltype(ii)::value;
-        q[col % 4] = fma(A[col], xs[ii], q[col % 4]);
-      });
+    double R[4], W[4];
+    rep4(l > j1 ? x : l == j1 ? amb : 0.0, R);
+    // A v = scal * sum_{c >= j+1} A(:, c) xt_c, eight chains (volatile forms in this order: a
+    // chain's FMAs eight instructions apart, past the DPP read-after-write wait states)
+    double q[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    sfor<KT - 8 * gb>([&](auto cc) {
+      constexpr int col = 8 * gb + decltype(cc)::value;
+      q[col % 8] = fmac_row_v<col % 16>(q[col % 8], R[col / 16], A[col]);
     });
-    const double av = scal * ((q[0] + q[1]) + (q[2] + q[3]));  // (A v)_l
+    const double av =
+        scal * (((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7])));  // (A v)_l
     const double s1 = tau * wave_sum_dpp(v * av);   // v^T (tau A v); v = 0 at rows <= j
     const double wl = l > jl ? fma(-0.5 * tau * s1, v, tau * av) : 0.0;
     const double wsl = wl * scal;
-    sm.wrow[l] = wl;
-    __syncthreads();
-    // A <- A - v w^T - w v^T; xt_c and w_c from LDS (broadcast reads)
+    rep4(wl, W);
+    // A <- A - w v^T - v w^T, a group's eight columns per pass (each column's second FMA
+    // eight instructions after its first)
     sfor<NG - gb>([&](auto gg) {
       constexpr int c0 = 8 * (gb + decltype(gg)::value);
-      double wc[8], xs[8];
-      row8(sm.wrow, c0, wc);
-      row8(sm.row, c0, xs);
       sfor<8>([&](auto ii) {
         constexpr int col = c0 + decltype(ii)::value;
-        A[col] = fma(-v, wc[ii], fma(-wsl, xs[ii], A[col]));
+        A[col] = fnmac_row_v<col % 16>(A[col], R[col / 16], wsl);
+      });
+      sfor<8>([&](auto ii) {
+        constexpr int col = c0 + decltype(ii)::value;
+        A[col] = fnmac_row_v<col % 16>(A[col], W[col / 16], v);
       });
     });
   };
@@ -215,9 +239,9 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   });
   {  // the trailing 2x2 (rows k-2, k-1): already tridiagonal
     const int jl = nst;
-    publish_row(jl, false);
+    publish_row(jl);
     const double d0 = sm.row[jl], e1 = sm.row[jl + 1];
-    publish_row(jl + 1, false);
+    publish_row(jl + 1);
     const double d1 = sm.row[jl + 1];
     trace += d0;
     trace += d1;

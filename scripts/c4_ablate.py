@@ -1,0 +1,56 @@
+"""Timing ablations of the k = 128 paths on C4: per-kernel ms per launch at each
+CWBL_DEBUG_TQ_STOP[:CWBL_DEBUG_TQ_STEPS] setting.  Needs the DEBUG_KNOBS library (`make -C
+cwbnwp-letkf_amd debuglib`, loaded with CWBL_LIBRARY=cwbnwp-letkf_amd/lib_dbg/libcwbl.so); the
+release library ignores the variables.
+
+  --path 2 (two-stage band path; head: 1 assembly only, 5 without the panel QRs, 6 the QRs
+            without the trailing updates; tail: 2 the chase only, 3 chase + quadrature)
+  --path 1 (hand-off path; hand-off kernel: 12 column staging only, 1 assembly only, 0:S the
+            first S of its 64 steps; tail kernel: 2 its steps only, 3 steps + quadrature)
+
+Usage: python scripts/c4_ablate.py [--path N] [stop[:steps] ...]"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, "cwbnwp-letkf_amd")
+import torch  # noqa: E402
+
+from cwbl import abi, dist as cdist, synth  # noqa: E402
+
+args = sys.argv[1:]
+path = 2
+if args[:1] == ["--path"]:
+    path, args = int(args[1]), args[2:]
+specs = args or (["0", "1", "5", "6", "2", "3"] if path == 2 else ["0", "12", "1", "0:16", "0:32",
+                                                                   "0:48", "2", "3"])
+w = synth.make("c4", local_noise=True)
+dev = torch.device("cuda:0")
+types = [dict(family=1, type_id=w.radar_type, xyz=w.obs_xyz, obs=w.obs, hdxb=w.hdxb)]
+_, types = cdist.unpack_obs_set(torch.from_numpy(cdist.pack_obs_set(types, w.k)).to(dev))
+x, y, alt = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt))
+var0 = torch.from_numpy(w.var).to(dev)
+core = abi.Core(w.k, device=0, options={"big_path": path})
+core.set_obs(cdist.builder_from(types, abi.MEM_DEVICE).build())
+var = var0.clone()
+slab = abi.make_slab(x, y, alt, var, memory=abi.MEM_DEVICE)
+for spec in specs:
+    stop, _, steps = spec.partition(":")
+    os.environ["CWBL_DEBUG_TQ_STOP"] = stop
+    os.environ["CWBL_DEBUG_TQ_STEPS"] = steps or "0"
+    var.copy_(var0)
+    core.analyze_var(w.vp, slab)
+    core.set_kernel_timing(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    var.copy_(var0)
+    core.analyze_var(w.vp, slab)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kt = core.kernel_times()
+    core.set_kernel_timing(False)
+    print(spec, json.dumps({"ms_per_var": round(el * 1e3, 1),
+                            "kernels": {k: round(v["ms"] / max(v["launches"], 1), 3)
+                                        for k, v in kt.items() if "search" not in k}}), flush=True)
+core.finalize()
