@@ -413,7 +413,8 @@ std::string kernel_name(int id) {
     case KT_BIG_HANDOFF:
       return "solve_tq_big_kernel<" + kp + ", false, " + std::to_string(big_split_j0(S.kp)) + ">";
     case KT_TQB_TAIL:
-      return "solve_tqb_tail_kernel<" + kp + ", " + std::to_string(big_split_j0(S.kp)) + ", 2>";
+      return "solve_tqb_tail_kernel<" + kp + ", " + std::to_string(big_split_j0(S.kp)) +
+             (S.kp == 128 ? ", 3>" : ", 2>");
     case KT_SOLVE_TQ: return "solve_tq_kernel<" + kp + ", false>";
     case KT_SOLVE_TQ_BIG: return "solve_tq_big_kernel<" + kp + ", false>";
     case KT_SOLVE_JACOBI: return "solve_kernel<" + kp + ", false>";

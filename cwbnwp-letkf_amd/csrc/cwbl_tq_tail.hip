@@ -464,9 +464,11 @@ hipError_t launch_solve_tqb_tail(hipStream_t s, int kp, SolveConsts c, SlabDev s
                                  long long g0, int npts, double *ws, int2 *info) {
   if (npts <= 0) return hipSuccess;
   if (c.quad == nullptr || (kp != 96 && kp != 128) || c.k <= kp - 62) return hipErrorInvalidValue;
-  // (3 waves per SIMD, 168 VGPRs, spills 35 registers: 2.88 s per C4 variable against 2.57)
+  // (KP = 128 at three waves per SIMD: 168 VGPRs, a few spills outside the step loop; 5.2 ms
+  // per 77.6 k-point launch against 5.8 at two.  Loading the back-transform's reflectors three
+  // groups ahead instead of one measured 5.8 ms.)
   if (kp == 128)
-    hipLaunchKernelGGL((solve_tqb_tail_kernel<128, 64, 2>), dim3(npts), dim3(64), 0, s, c, slab,
+    hipLaunchKernelGGL((solve_tqb_tail_kernel<128, 64, 3>), dim3(npts), dim3(64), 0, s, c, slab,
                        g0, npts, ws, info);
   else
     hipLaunchKernelGGL((solve_tqb_tail_kernel<96, 32, 2>), dim3(npts), dim3(64), 0, s, c, slab,

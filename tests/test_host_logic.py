@@ -130,7 +130,7 @@ def test_roofline_block_takes_the_dominant_kernel_and_its_algorithmic_flops():
     assert abs(tq - solved * (tri + 6 * k * k) / 2e-3 / 1e12) < 1e-9
     # the split k = 128 pair: steps 0..63 in the hand-off kernel, the rest in the tail
     a = bench.kernel_algorithmic_flops("solve_tq_big_kernel<128, false, 64>", 128, 1, 200)
-    b = bench.kernel_algorithmic_flops("solve_tqb_tail_kernel<128, 64, 2>", 128, 1, 200)
+    b = bench.kernel_algorithmic_flops("solve_tqb_tail_kernel<128, 64, 3>", 128, 1, 200)
     assert a + b == 200 * (128 * 129 + 256) + bench._tri_flops(128, 0, 128) + 6 * 128 * 128
     # the two-stage band pair prices the same algorithm
     c = bench.kernel_algorithmic_flops("band_head_kernel<false>", 128, 1, 200)
