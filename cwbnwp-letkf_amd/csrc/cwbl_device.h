@@ -716,6 +716,15 @@ __device__ __forceinline__ int stage_columns_pipe(
     };
     auto gather = [&](int base, int slot, Gath &G) {
       G.live = sl < min(CHUNK, npairs - base);
+      if (CWBL_DBG_STOP(c) == 13) {  // timing ablation: the assembly without the gathers
+#pragma unroll
+        for (int i = 0; i < VH / 2; ++i) G.g[i] = f32x4{1.0f, 1.0f, 1.0f, 1.0f};
+        G.rd = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        G.err = 1.0f;
+        G.omm = 0.0f;
+        G.okb = 1;
+        return;
+      }
       const int q = base + sl;
       const int jn = divn(q), v = q - jn * nvar;
       const int col = slot * nvar + v;  // a valid table index even past the list (slot 0)

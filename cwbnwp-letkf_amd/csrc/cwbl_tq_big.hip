@@ -320,7 +320,7 @@ solve_tq_big_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev s
     return;
   }
 
-  if (CWBL_DBG_STOP(c) == 1 || CWBL_DBG_STOP(c) == 12) {  // timing ablation: assembly only
+  if (CWBL_DBG_STOP(c) == 1 || CWBL_DBG_STOP(c) >= 12) {  // timing ablation: assembly only
     double t = b1acc;
 #pragma unroll
     for (int it = 0; it < NBL; ++it)
