@@ -500,6 +500,9 @@ def kernel_algorithmic_flops(name, k, solved, nobs_sum):
     if name.startswith("solve_tq_big_kernel") and name.count(",") == 2:  # hand-off kernel
         j0 = int(name.split(",")[2].strip(" >"))
         return syrk + solved * _tri_flops(k, 0, j0)
+    if name.startswith("solve_tq_rows_kernel"):  # half-row hand-off kernel <KP, J0>
+        j0 = int(name.split(",")[1].strip(" >"))
+        return syrk + solved * _tri_flops(k, 0, j0)
     if name.startswith("solve_tqb_tail_kernel"):
         j0 = int(name.split(",")[1].strip(" >"))
         return solved * _tri_flops(k, j0, k) + vec

@@ -411,7 +411,9 @@ std::string kernel_name(int id) {
     case KT_ASSEMBLE_RECORD: return "assemble_record_kernel<" + std::to_string(kRecordWaves) + ">";
     case KT_SOLVE_TQ40: return "solve_tq40_kernel<" + kp + ", 0>";
     case KT_BIG_HANDOFF:
-      return "solve_tq_big_kernel<" + kp + ", false, " + std::to_string(big_split_j0(S.kp)) + ">";
+      return S.kp == 128 ? "solve_tq_rows_kernel<128, 64>"
+                         : "solve_tq_big_kernel<" + kp + ", false, " +
+                               std::to_string(big_split_j0(S.kp)) + ">";
     case KT_TQB_TAIL:
       return "solve_tqb_tail_kernel<" + kp + ", " + std::to_string(big_split_j0(S.kp)) +
              (S.kp == 128 ? ", 3>" : ", 2>");

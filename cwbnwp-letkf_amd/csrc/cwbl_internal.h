@@ -246,6 +246,10 @@ struct BigHandoff {
 hipError_t launch_big_handoff(hipStream_t s, int kp, const TreeDesc *trees, SolveConsts c,
                               SlabDev slab, long long g0, int npts, const int *nbr_cnt,
                               const int *nbr_idx, int2 *info, double *ws);
+// KP = 128: the half-row hand-off kernel (cwbl_tq_rows.hip), launched by launch_big_handoff
+hipError_t launch_rows_handoff(hipStream_t s, const TreeDesc *trees, SolveConsts c, SlabDev slab,
+                               long long g0, int npts, const int *nbr_cnt, const int *nbr_idx,
+                               int2 *info, double *ws);
 hipError_t launch_solve_tqb_tail(hipStream_t s, int kp, SolveConsts c, SlabDev slab,
                                  long long g0, int npts, double *ws, int2 *info);
 

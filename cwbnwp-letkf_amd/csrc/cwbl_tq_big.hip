@@ -850,10 +850,10 @@ hipError_t launch_big_handoff(hipStream_t s, int kp, const TreeDesc *trees, Solv
                               const int *nbr_idx, int2 *info, double *ws) {
   if (npts <= 0) return hipSuccess;
   if ((kp != 96 && kp != 128) || c.k <= kp - 62) return hipErrorInvalidValue;
-  if (kp == 128)  // hand-off after kp - 64 steps: 64 trailing rows, one per tail lane
-    hipLaunchKernelGGL((solve_tq_big_kernel<128, false, 64>), dim3(npts), dim3(kBigThreads), 0,
-                       s, trees, c, slab, g0, npts, nbr_cnt, nbr_idx, nullptr, nullptr, nullptr,
-                       nullptr, nullptr, info, ws);
+  // hand-off after kp - 64 steps: 64 trailing rows, one per tail lane.  KP = 128 runs the
+  // half-row kernel (cwbl_tq_rows.hip): two barriers per step against this kernel's four
+  if (kp == 128)
+    return launch_rows_handoff(s, trees, c, slab, g0, npts, nbr_cnt, nbr_idx, info, ws);
   else
     hipLaunchKernelGGL((solve_tq_big_kernel<96, false, 32>), dim3(npts), dim3(kBigThreads), 0,
                        s, trees, c, slab, g0, npts, nbr_cnt, nbr_idx, nullptr, nullptr, nullptr,
