@@ -196,6 +196,29 @@ __device__ __forceinline__ double rsum8(double v) {
   return v;
 }
 
+// ---- per-point records through a buffer resource ----------------------------------------
+// A lane whose byte offset is kRecSkip (past any record) loads 0 and stores nothing, with no
+// memory access: triangular parts of a record are masked without branches (a branch around
+// a load leaves the wait for it on the skipping path) and without moving their zero bytes.
+constexpr unsigned kRecSkip = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rec_rsrc(const double *base, int words) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base), 0, words * 8, 0x00020000);
+}
+// word w of the record, or kRecSkip
+__device__ __forceinline__ unsigned rec_off(bool live, int w) {
+  return live ? 8u * (unsigned)w : kRecSkip;
+}
+__device__ __forceinline__ double rec_ld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+  return __longlong_as_double(((long long)v[1] << 32) | (unsigned)v[0]);
+}
+__device__ __forceinline__ void rec_st(__amdgpu_buffer_rsrc_t r, unsigned off, double x) {
+  const long long b = __double_as_longlong(x);
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 v = {(unsigned)b, (unsigned)(b >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 0);
+}
+
 // v through a register the compiler cannot see through, after `dep` is known.  The per-row
 // LDS offsets of a quadrature walk whose direction differs per lane (base + dir * t) are
 // loop-invariant: without this the compiler hoists all of them out of the pass loop and holds

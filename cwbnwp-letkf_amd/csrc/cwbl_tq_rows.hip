@@ -5,11 +5,12 @@
 // the reference's dsyevd reduction, module_eigen.f90:48-56), handed over through the
 // workspace (BigHandoff<128, 64>) to solve_tqb_tail_kernel (cwbl_tq_tail.hip).
 //
-// One 256-thread workgroup per grid point, the matrix held in HALF ROWS: wave w holds rows
-// 64 (w / 2) + lane, columns 64 (w % 2) .. 64 (w % 2) + 63, both triangles (A is kept
-// symmetric).  A step then needs no LDS traffic beyond three vectors:
-//   - the pivot column (half-0 waves: each lane's own entry A[j], picked by value) goes to
-//     LDS with its norm partials (barrier A);
+// One 256-thread workgroup per grid point, the matrix held in HALF ROWS: wave w holds row
+// 64 (w / 2) + lane, the columns of half h = w % 2 (the 8-column groups 2 i + h: dead columns
+// leave both halves at the same rate), both triangles (A is kept symmetric).  A step then
+// needs no LDS traffic beyond three vectors:
+//   - the pivot column (the waves of the half holding column j: each lane's own entry,
+//     picked by value) goes to LDS with its norm partials (barrier A);
 //   - every lane copies the 64 pivot-row entries of its half into four row-replicated
 //     registers (four LDS reads) and runs the matvec as row_newbcast operands of fused
 //     v_fmac_f64_dpp, as the tail kernel does; the half-row partials of A v and the partial
@@ -17,9 +18,9 @@
 //   - every lane forms w for its replicated columns from the two partials (no third
 //     exchange) and runs the rank-2 update the same way.
 // Two barriers per step (the 4x4-block kernel, solve_tq_big_kernel, needs four and moves its
-// block partials and both vectors through LDS each step).  The half-0 waves' steps run in
-// compile-time blocks by the 8-column group of column j + 1, so their dead columns (c <= j)
-// are skipped statically; the half-1 waves' columns (64..127) stay live for all 64 steps.
+// block partials and both vectors through LDS each step).  The steps run in compile-time
+// blocks by the 8-column group of column j + 1, so the dead columns (c <= j) are skipped
+// statically.
 #include "cwbl_device.h"
 
 #include <type_traits>
@@ -35,6 +36,9 @@ constexpr int kRowsKP = 128, kRowsHS = 64, kRowsChunk = 32;
 __device__ __forceinline__ int tile_at(int i, int jj) { return 16 * i + (jj ^ ((i >> 1) & 7)); }
 // lower-triangle tile index of tile (I, J), I >= J
 __device__ __forceinline__ int tile_index(int I, int J) { return I * (I + 1) / 2 + J; }
+// the column of local column cc of half h: half h holds the 8-column groups 2 i + h, so the
+// dead columns (c <= j) leave both halves at the same rate
+__host__ __device__ constexpr int gcol(int h, int cc) { return 16 * (cc >> 3) + 8 * h + (cc & 7); }
 
 }  // namespace
 
@@ -172,13 +176,13 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
   }
   __syncthreads();
   double ux = sm.x[r], ub = sm.p[0][r];  // x', then Q^T x'; b1, then Q^T b1 (row r)
-  // half row: A[cc] = A(r, 64 h + cc)
+  // half row: A[cc] = A(r, gcol(h, cc))
   double A[64];
   {
     const int I = r >> 4, i = r & 15;
     sfor<64>([&](auto CC_) {
       constexpr int cc = decltype(CC_)::value;
-      const int col = 64 * h + cc, J = col >> 4, jj = col & 15;
+      const int col = gcol(h, cc), J = col >> 4, jj = col & 15;
       A[cc] = I >= J ? sm.u.tl[tile_index(I, J)][tile_at(i, jj)]
                      : sm.u.tl[tile_index(J, I)][tile_at(jj, i)];
     });
@@ -192,6 +196,7 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
   }
 
   double *__restrict__ wo = ws + (long long)gi * HO::WORDS;
+  const auto rec = rec_rsrc(wo, HO::WORDS);
   auto opq = [](double a) {  // (see the tail kernel: picks by value, no scratch)
     asm("" : "+v"(a));
     return a;
@@ -204,18 +209,28 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
 
   // ---- Householder steps j = 0 .. 63 ----------------------------------------------------------
   // C0: the first live column of this wave's half (static; 0 for half 1)
-  auto step = [&](const int j, auto C0, auto HALF0) {
-    constexpr int c0 = decltype(C0)::value;
-    constexpr bool half0 = decltype(HALF0)::value;
+  // Block GJ: the steps whose column j + 1 is in group gj (j = 8 gj - 1 .. 8 gj + 6); H: this
+  // wave's half (static); c0: its first live local column in the block
+  auto step = [&](const int j, auto GJ, auto H) {
+    constexpr int gj = decltype(GJ)::value, hh = decltype(H)::value;
+    constexpr int i0 = (gj - hh + 1) >> 1 > 0 ? (gj - hh + 1) >> 1 : 0, c0 = 8 * i0;
+    constexpr bool half0 = hh == 0;
     const int j1 = j + 1;
-    // phase A: the pivot column and x.x (half-0 waves)
-    if constexpr (half0) {
-      constexpr int jb = c0 == 0 ? 0 : c0 - 1;  // the block's first step
-      double xr = opq(A[jb]);
-      sfor<7>([&](auto ii) {
-        constexpr int cc = jb + 1 + decltype(ii)::value;
-        if constexpr (cc < 64) xr = j == cc ? opq(A[cc]) : xr;
-      });
+    // phase A: the pivot column and x.x, from the half holding column j (its entries A[cc],
+    // picked by value among the block's candidates: columns 8 gj .. 8 gj + 6 if group gj is
+    // this half's, column 8 gj - 1 if group gj - 1 is)
+    if (((j >> 3) & 1) == hh) {
+      double xr = 0.0;
+      if constexpr ((gj & 1) == hh) {
+        sfor<7>([&](auto ee) {
+          constexpr int e = decltype(ee)::value, cc = 8 * (gj >> 1) + e;
+          if constexpr (cc < 64) xr = j == 8 * gj + e ? opq(A[cc]) : xr;
+        });
+      }
+      if constexpr (gj >= 1 && ((gj - 1) & 1) == hh) {
+        constexpr int cc = 8 * ((gj - 1) >> 1) + 7;
+        xr = j == 8 * gj - 1 ? opq(A[cc]) : xr;
+      }
       sm.x[r] = xr;
       const double xs = wave_sum_dpp(r > j1 ? xr * xr : 0.0);
       if (l == 0) sm.redA[rb] = xs;
@@ -240,12 +255,13 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
     }
     const double xo = sm.x[r];
     const double v = r == j1 ? 1.0 : r > j1 ? xo * scal : 0.0;
-    if constexpr (half0) wo[HO::HV + j * KP + r] = v;  // reflector j (1 at row j + 1)
+    // reflector j, rows > j (1 at row j + 1; the tail kernel loads no row above)
+    if constexpr (half0) rec_st(rec, rec_off(r > j, HO::HV + j * KP + r), v);
     double R[4];
     sfor<4>([&](auto G) {
       constexpr int g = decltype(G)::value;
       if constexpr (16 * g + 15 >= c0) {
-        const int cc = 64 * h + 16 * g + (l & 15);
+        const int cc = gcol(hh, 16 * g + (l & 15));
         const double xc = sm.x[cc];
         R[g] = cc > j1 ? xc : cc == j1 ? amb : 0.0;
       } else {
@@ -283,7 +299,7 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
     sfor<4>([&](auto G) {
       constexpr int g = decltype(G)::value;
       if constexpr (16 * g + 15 >= c0) {
-        const int cc = 64 * h + 16 * g + (l & 15);
+        const int cc = gcol(hh, 16 * g + (l & 15));
         W[g] = cc > j ? fma(hs, scal * R[g], tau * (sm.p[0][cc] + sm.p[1][cc])) : 0.0;
       } else {
         W[g] = 0.0;
@@ -302,24 +318,22 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
       });
     });
   };
-  if (h == 0) {
-    // block gb: steps j = 8 gb - 1 .. 8 gb + 6 (column j + 1 in group gb)
-    sfor<8>([&](auto GB) {
-      constexpr int gb = decltype(GB)::value;
-      for (int j = gb == 0 ? 0 : 8 * gb - 1; j <= 8 * gb + 6; ++j)
-        step(j, std::integral_constant<int, 8 * gb>{}, std::true_type{});
+  // (debug_steps: timing ablation, the first steps only)
+  const int jend = CWBL_DBG_STEPS(c) > 0 ? min(HS, CWBL_DBG_STEPS(c)) : HS;
+  auto run = [&](auto H) {
+    sfor<9>([&](auto GJ) {  // j + 1 <= 64: groups 0 .. 8
+      constexpr int gj = decltype(GJ)::value;
+      for (int j = gj == 0 ? 0 : 8 * gj - 1; j <= min(8 * gj + 6, jend - 1); ++j) step(j, GJ, H);
     });
-    // step 63: column 64 is the half-1 waves' first; nothing of half 0 is live
-    step(HS - 1, std::integral_constant<int, 64>{}, std::true_type{});
-  } else {
-    for (int j = 0; j < HS; ++j) step(j, std::integral_constant<int, 0>{}, std::false_type{});
-  }
+  };
+  if (h == 0) run(std::integral_constant<int, 0>{});
+  else run(std::integral_constant<int, 1>{});
 
   // ---- hand-off (BigHandoff): the trailing 64x64 (wave 3's half rows), Q^T b1, Q^T x', T ----
-  if (wave == 3) {
-    sfor<64>([&](auto CC_) {
-      constexpr int cc = decltype(CC_)::value;
-      wo[HO::TA + cc * HO::KT + l] = A[cc];  // (r, c) at c KT + r
+  if (rb == 1) {  // columns 64..127: local columns 32..63 of either half
+    sfor<32>([&](auto CC_) {
+      constexpr int cc = 32 + decltype(CC_)::value;
+      wo[HO::TA + (gcol(h, cc) - 64) * HO::KT + l] = A[cc];  // (r, c) at c KT + r
     });
   }
   if (h == 0) {

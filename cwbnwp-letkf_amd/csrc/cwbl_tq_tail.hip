@@ -125,7 +125,8 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   };
   // the record's scratch rows (BT): row jl of this kernel's steps, where the back-transform
   // finds it once the registers are released
-  double *__restrict__ parked = ws + (long long)gi * HO::WORDS + HO::BT;
+  // (entries at or above the reflector's row j + 1 are neither stored nor loaded: rec_off)
+  const auto rec = rec_rsrc(ws + (long long)gi * HO::WORDS, HO::WORDS);
 
   // ---- Householder steps j = J0 .. k-3 (local jl = j - J0) --------------------------------
   // A is symmetric, so lane l's entry A[jl] is the pivot row's entry l.  The pivot row and w
@@ -173,7 +174,7 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       constexpr int cc = jb + 1 + decltype(ii)::value;
       if constexpr (cc < KT) xr = jl == cc ? opq(A[cc]) : xr;
     });
-    parked[jl * KT + l] = xr;
+    rec_st(rec, rec_off(l > j1, HO::BT + jl * KT + l), xr);
     const double dj = readlane_f64(xr, jl), alpha = readlane_f64(xr, j1);
     trace += dj;
     const double x = l > j1 ? xr : 0.0;
@@ -375,7 +376,7 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     sfor<4>([&](auto qq) {
       const int jl = top - 3 + qq;  // < 0: padding (H = I)
       const int j1 = jl + 1;
-      const double xr = parked[(jl < 0 ? 0 : jl) * KT + l];
+      const double xr = rec_ld(rec, rec_off(jl >= 0 && l > j1, HO::BT + jl * KT + l));
       const double sc = sm.scl[J0 + (jl < 0 ? 0 : jl)];
       v1[qq] = jl < 0 ? 0.0 : l == j1 ? 1.0 : (l > j1 ? sc * xr : 0.0);
       ta[qq] = jl < 0 ? 0.0 : sm.tau[J0 + jl];
@@ -384,8 +385,8 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   auto load_hand = [&](int top, double (&v0)[4], double (&v1)[4], double (&ta)[4]) {
     sfor<4>([&](auto qq) {
       const int j = top - 3 + qq;
-      const double h0 = w[HO::HV + j * KP + l];
-      v0[qq] = mem0 && l > j ? h0 : 0.0;  // row j + 1 holds 1.0
+      // rows <= j hold zeros (not loaded); row j + 1 holds 1.0
+      v0[qq] = rec_ld(rec, rec_off(mem0 && l > j, HO::HV + j * KP + l));
       v1[qq] = w[HO::HV + j * KP + J0 + l];
       ta[qq] = sm.tau[j];
     });
