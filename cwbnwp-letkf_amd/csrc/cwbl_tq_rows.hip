@@ -208,34 +208,30 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
   };
 
   // ---- Householder steps j = 0 .. 63 ----------------------------------------------------------
-  // C0: the first live column of this wave's half (static; 0 for half 1)
+  // Phase A of step jn: column jn (in group gjn, held by half gjn & 1 as its local columns
+  // 8 (gjn / 2) ..) and x.x below row jn + 1 to LDS.  It runs inside the previous step's
+  // update, right after the group holding the column is updated, so its reductions overlap
+  // the rest of the update (nobody reads x or redA between barrier B and the next barrier A).
+  auto phase_a = [&](int jn, auto GJN) {
+    constexpr int gjn = decltype(GJN)::value;
+    double xr = 0.0;
+    sfor<8>([&](auto ee) {
+      constexpr int e = decltype(ee)::value, cc = 8 * (gjn >> 1) + e;
+      xr = jn == 8 * gjn + e ? opq(A[cc]) : xr;
+    });
+    sm.x[r] = xr;
+    const double xs = wave_sum_dpp(r > jn + 1 ? xr * xr : 0.0);
+    if (l == 0) sm.redA[rb] = xs;
+  };
   // Block GJ: the steps whose column j + 1 is in group gj (j = 8 gj - 1 .. 8 gj + 6); H: this
   // wave's half (static); c0: its first live local column in the block
+  const int jend = CWBL_DBG_STEPS(c) > 0 ? min(HS, CWBL_DBG_STEPS(c)) : HS;  // (ablation)
   auto step = [&](const int j, auto GJ, auto H) {
     constexpr int gj = decltype(GJ)::value, hh = decltype(H)::value;
     constexpr int i0 = (gj - hh + 1) >> 1 > 0 ? (gj - hh + 1) >> 1 : 0, c0 = 8 * i0;
     constexpr bool half0 = hh == 0;
     const int j1 = j + 1;
-    // phase A: the pivot column and x.x, from the half holding column j (its entries A[cc],
-    // picked by value among the block's candidates: columns 8 gj .. 8 gj + 6 if group gj is
-    // this half's, column 8 gj - 1 if group gj - 1 is)
-    if (((j >> 3) & 1) == hh) {
-      double xr = 0.0;
-      if constexpr ((gj & 1) == hh) {
-        sfor<7>([&](auto ee) {
-          constexpr int e = decltype(ee)::value, cc = 8 * (gj >> 1) + e;
-          if constexpr (cc < 64) xr = j == 8 * gj + e ? opq(A[cc]) : xr;
-        });
-      }
-      if constexpr (gj >= 1 && ((gj - 1) & 1) == hh) {
-        constexpr int cc = 8 * ((gj - 1) >> 1) + 7;
-        xr = j == 8 * gj - 1 ? opq(A[cc]) : xr;
-      }
-      sm.x[r] = xr;
-      const double xs = wave_sum_dpp(r > j1 ? xr * xr : 0.0);
-      if (l == 0) sm.redA[rb] = xs;
-    }
-    __syncthreads();
+    __syncthreads();  // barrier A: column j and its x.x are in LDS
     // phase B: the reflector, v, the replicated pivot row, the matvec
     const double xn2 = sm.redA[0] + sm.redA[1];
     const double dj = sm.x[j], alpha = sm.x[j1];
@@ -307,7 +303,7 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
     });
     pin4(W);
     sfor<(64 - c0) / 8>([&](auto GG) {
-      constexpr int cb = c0 + 8 * decltype(GG)::value;
+      constexpr int gg = decltype(GG)::value, cb = c0 + 8 * gg;
       sfor<8>([&](auto ii) {
         constexpr int cc = cb + decltype(ii)::value;
         A[cc] = fnmac_row_v<cc % 16>(A[cc], R[cc / 16], wsl);
@@ -316,10 +312,14 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
         constexpr int cc = cb + decltype(ii)::value;
         A[cc] = fnmac_row_v<cc % 16>(A[cc], W[cc / 16], v);
       });
+      // column j + 1 (group gj, the first live group of half gj & 1) is final: phase A of the
+      // next step
+      if constexpr (gg == 0 && hh == (gj & 1) && gj < 8) {
+        if (j1 < jend) phase_a(j1, GJ);
+      }
     });
   };
-  // (debug_steps: timing ablation, the first steps only)
-  const int jend = CWBL_DBG_STEPS(c) > 0 ? min(HS, CWBL_DBG_STEPS(c)) : HS;
+  if (h == 0) phase_a(0, std::integral_constant<int, 0>{});  // column 0: half 0, group 0
   auto run = [&](auto H) {
     sfor<9>([&](auto GJ) {  // j + 1 <= 64: groups 0 .. 8
       constexpr int gj = decltype(GJ)::value;
