@@ -115,15 +115,16 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
           tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(t <= wave ? a : b, (double)ys[offJx[t]],
                                                          tile[t], 0, 0, 0);
       }
-      if (tid < KP) {  // Yb d: eight columns per round, four chains
+      {  // Yb d: row tid % 128, the rounds of eight columns split between the two thread
+         // halves (all four waves take a share), four chains
         const int nr = (nsl + 7) / 8;
-        for (int r8 = 0; r8 < nr; ++r8) {
+        for (int r8 = tid >> 7; r8 < nr; r8 += 2) {
           const float4 o0 = *reinterpret_cast<const float4 *>(&cb.yo[8 * r8]);
           const float4 o1 = *reinterpret_cast<const float4 *>(&cb.yo[8 * r8 + 4]);
           const float o[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
           float y[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) y[i] = cb.at(8 * r8 + i, tid);
+          for (int i = 0; i < 8; ++i) y[i] = cb.at(8 * r8 + i, tid & 127);
 #pragma unroll
           for (int i = 0; i < 8; ++i) b1p[i & 3] = fma((double)y[i], (double)o[i], b1p[i & 3]);
         }
@@ -170,12 +171,10 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
     return sm.parf * c.nmember_inv;
   }();
   const double xb_mean = (double)xb_mean_f;
-  if (tid < KP) {
-    sm.x[tid] = tid < k ? (double)xbl - xb_mean : 0.0;
-    sm.p[0][tid] = b1acc;
-  }
+  if (tid < KP) sm.x[tid] = tid < k ? (double)xbl - xb_mean : 0.0;
+  sm.p[tid >> 7][tid & 127] = b1acc;  // the two halves' Yb d partials
   __syncthreads();
-  double ux = sm.x[r], ub = sm.p[0][r];  // x', then Q^T x'; b1, then Q^T b1 (row r)
+  double ux = sm.x[r], ub = sm.p[0][r] + sm.p[1][r];  // x', then Q^T x'; b1, then Q^T b1
   // half row: A[cc] = A(r, gcol(h, cc))
   double A[64];
   {
