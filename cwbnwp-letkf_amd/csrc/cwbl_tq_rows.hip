@@ -29,7 +29,9 @@ namespace cwbl {
 
 namespace {
 
-constexpr int kRowsKP = 128, kRowsHS = 64, kRowsChunk = 32;
+// (64-column chunks: a chunk's MFMA phase at two waves per SIMD then covers the next chunk's
+// gathers; the staging shares its LDS with the 72 KB tile area, so they cost no occupancy)
+constexpr int kRowsKP = 128, kRowsHS = 64, kRowsChunk = 64;
 
 // element (i, jj) of a staged 16x16 tile: rows of 16 doubles, the column XOR-rotated by the
 // row pair so that 16 lanes reading one column of a tile (rows i) hit 32 distinct banks
