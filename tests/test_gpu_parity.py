@@ -610,12 +610,14 @@ def test_large_ensemble_block_vs_oracle(k):
 @pytest.mark.parametrize("k,sparse", [(65, False), (80, True), (96, False), (97, False),
                                       (101, True), (127, False), (128, False), (128, True)])
 def test_split_big_path_vs_one_kernel_and_oracle(k, sparse):
-    """The KP = 96 / 128 slab paths run split by default: solve_tq_big_kernel<KP, false,
-    KP - 64> (256 threads per point) hands the trailing 64x64 matrix and its reflectors to
-    solve_tqb_tail_kernel (one point per wavefront).  k < KP exercises the identity padding;
-    the sparse obs set gives points with p < k (rank-deficient Yb Yb^T, exactly-zero
-    reflectors, tau = 0).  Against the one-kernel path (big_path = 0) on the whole
-    30x30x50 grid and the oracle on a 5x5-column block; hand-off batches of 1024 points."""
+    """The KP = 96 / 128 slab paths run split by default: a 256-thread kernel per point
+    (solve_tq_big_kernel<96, false, 32>, 4x4 register blocks; solve_tq_rows_kernel<128, 64>,
+    half rows) hands the trailing 64x64 matrix and its reflectors to solve_tqb_tail_kernel
+    (one point per wavefront); the kernel timing names the launched pair.  k < KP exercises
+    the identity padding; the sparse obs set gives points with p < k (rank-deficient
+    Yb Yb^T, exactly-zero reflectors, tau = 0).  Against the one-kernel path (big_path = 0)
+    on the whole 30x30x50 grid and the oracle on a 5x5-column block; hand-off batches of
+    1024 points."""
     import ctypes as C
     from cwbl import synth
     w = synth.make("c4", scale=0.1, k=k)
@@ -630,8 +632,16 @@ def test_split_big_path_vs_one_kernel_and_oracle(k, sparse):
         c = abi.Core(w.k, device=0, options={"big_batch": 1024, "big_path": int(mode)})
         c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
         var = w.var.copy()
+        c.set_kernel_timing(True)
         st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+        kt = c.kernel_times()
         c.finalize()
+        if mode == "1":
+            pair = (["solve_tq_rows_kernel<128, 64>", "solve_tqb_tail_kernel<128, 64, 3>"]
+                    if k > 96 else
+                    ["solve_tq_big_kernel<96, false, 32>", "solve_tqb_tail_kernel<96, 32, 2>"])
+            for name in pair:
+                assert kt.get(name, {}).get("launches", 0) > 0, (name, sorted(kt))
         assert np.isfinite(var).all()
         assert st.nonconverged == 0 and st.solved > 0
         out[mode] = (var, st.solved, st.nobs_sum)
