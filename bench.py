@@ -38,6 +38,7 @@ from cwbl.transpose import dims_create as tr_dims  # noqa: E402
 
 METRIC = "analysis grid-points/sec (+ wall-clock per cycle) at k=40, 1/2/4/8 MI355X"
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector = matrix on gfx950), spec
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
 def host_cores():
@@ -387,7 +388,9 @@ def time_config(name, rank, world, local, dev, steps, warmup):
     w = synth.make(name, shard=(rank, world) if world > 1 else None, local_noise=True)
     types = [dict(family=1, type_id=w.radar_type, xyz=w.obs_xyz, obs=w.obs, hdxb=w.hdxb)]
     if world > 1:
-        _, types = cdist.broadcast_obs_set(types if rank == 0 else None, w.k, dev, src=0)
+        # one RCCL broadcast: every rank knows the set's layout (the counts)
+        _, types = cdist.broadcast_obs_set(types if rank == 0 else None, w.k, dev, src=0,
+                                           layout=cdist.wire_layout(types))
     else:
         _, types = cdist.unpack_obs_set(torch.from_numpy(cdist.pack_obs_set(types, w.k)).to(dev))
     x, y, alt, var = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt, w.var))
@@ -412,6 +415,9 @@ def time_config(name, rank, world, local, dev, steps, warmup):
     nobs = sum(s.nobs_sum for s in stats)
     ms_solve = sum(s.ms_solve for s in stats)
     roof, per_kernel = roofline_block(ktimes, w.k, solved, nobs, ms_solve, name)
+    if roof is not None:
+        roof["hbm"] = hbm_block(name, w.k, float(sum(s.points for s in stats)) / steps,
+                                el / steps * 1e3)
     el, pts, sol, nsum = _max_over_ranks([el], world, dev) + _max_over_ranks(
         [float(sum(s.points for s in stats)), float(solved), float(nobs)], world, dev,
         dist.ReduceOp.SUM if world > 1 else None)
@@ -594,6 +600,34 @@ def roofline_block(ktimes, k, solved, nobs_sum, ms_solve, config):
     return roof, per
 
 
+def hbm_block(config, k, points_per_step, ms_per_step):
+    """The step's HBM fraction (north_star asks for the throughput "as fraction of the HBM
+    roofline"; SURVEY.md 8(d) says to report it beside the FP64 one): the PMC HBM bytes of
+    every kernel of one profiled step (profiles/pmc_kernels.json: FETCH_SIZE / WRITE_SIZE per
+    launch x launches, gfx950-corrected) / the live ms_per_step / 8 TB/s, and the unique-bytes
+    fraction 4 (2k + 3) B per point (xb in, xa out, coordinates) / ms_per_step / 8 TB/s."""
+    pmc, tag = load_pmc(config)
+    steps = max(int(pmc.get("_meta", {}).get("steps", 1)), 1)  # steps in the profiled run
+    kern = {n: e for n, e in pmc.items() if isinstance(e, dict) and "hbm_bytes_per_launch" in e}
+    if not kern or not ms_per_step:
+        return None
+    per_step = sum(e["hbm_bytes_per_launch"] * e.get("calls", 0) for e in kern.values()) / steps
+    sec = ms_per_step * 1e-3
+    uniq = 4.0 * (2 * k + 3) * points_per_step
+    return {"pmc_bytes_per_step": per_step,
+            "achieved_gbs": per_step / sec / 1e9,
+            "peak_gbs": HBM_PEAK_GBS,
+            "frac": per_step / sec / 1e9 / HBM_PEAK_GBS,
+            "unique_bytes_per_step": uniq,
+            "unique_gbs": uniq / sec / 1e9,
+            "unique_frac": uniq / sec / 1e9 / HBM_PEAK_GBS,
+            "by_kernel_bytes_per_step": {n: e["hbm_bytes_per_launch"] * e.get("calls", 0) / steps
+                                         for n, e in sorted(kern.items())},
+            "note": f"PMC bytes of every kernel of one profiled step ({tag}, "
+                    "profiles/pmc_kernels.json) over the live ms_per_step; the path is FP64-bound "
+                    "(SURVEY.md 8(d)), so neither fraction is the roofline it is held to"}
+
+
 def distinct_devices(world, dev):
     """GPUs the ranks run on (under gloo several ranks may share one)."""
     if world == 1:
@@ -707,7 +741,8 @@ def run(args, rank, world, stage):
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        _, types = cdist.broadcast_obs_set(types if rank == 0 else None, k, dev, src=0)
+        _, types = cdist.broadcast_obs_set(types if rank == 0 else None, k, dev, src=0,
+                                           layout=cdist.wire_layout(types))
         torch.cuda.synchronize()
         bcast_ms = (time.perf_counter() - t0) * 1e3
     else:
@@ -803,6 +838,9 @@ def run(args, rank, world, stage):
         ms_solve = sum(s.ms_solve for s in stats)
         ms_search = sum(s.ms_search for s in stats)
         roof, per_kernel = roofline_block(ktimes, k, solved, nobs_sum, ms_solve, args.config)
+        if roof is not None:
+            roof["hbm"] = hbm_block(args.config, k, pts_total / args.steps,
+                                    elapsed / args.steps * 1e3)
         hm = legs.get("host_memory") or {}
         pageable = hm.get("pageable") or {}
         out = {

@@ -190,6 +190,7 @@ struct ObsType {
 // depend on the variable's QC parameters).
 struct TreeBufs {
   int entry = -1, dim = 0, depth = 0;
+  int bin_div_opt = 0;  // CWBL_OPT_BIN_DIV the bins were built under
   float hinv = 0.0f, vinv = 0.0f;
   DevBuf nodes, rdata, ind, col_bg, col_omm, col_err, col_ok;
   DevBuf bxyz, bstart;  // uniform bins of the same coordinates (search_binned_kernel)
@@ -233,7 +234,10 @@ struct State {
   // batches keep each batch's lists and hand-off records nearer the caches and overlap
   // more of the search; below ~70 k the per-batch fixed costs win.
   long long max_batch = 160000;
-  bool max_batch_set = false;                         // CWBL_OPT_MAX_BATCH given: no ~6-batch rule
+  bool max_batch_set = false;
+  // one-stream path: the per-point info (solved, p) of a window of up to info_window points
+  // is reduced once per window (a reduction kernel per batch cost the C2 step ~0.5 ms)
+  long long info_window = 1LL << 25;  // 256 MB of int2 (CWBL_OPT_INFO_WINDOW)                         // CWBL_OPT_MAX_BATCH given: no ~6-batch rule
   DevBuf sx, sy, salt, svar;                          // slab staging (host-memory calls)
   DevBuf bcol, byo, byb, bxb, bxa, bev, btri;         // solve_batch staging (btri: T per point)
   DevBuf qxyz, qnf, qidx, qr2;                        // search staging
@@ -532,7 +536,7 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
     TreeBufs *tb = nullptr;
     for (auto &t : S.tree_cache)
       if (t->entry == pd.entry && t->dim == tdim && t->hinv == pd.hinv &&
-          (!dim3 || t->vinv == pd.vinv))
+          (!dim3 || t->vinv == pd.vinv) && t->bin_div_opt == S.bin_div)
         tb = t.get();
     if (!tb) {  // build_tree (:35-167) for this normalisation
       std::vector<float> nx(3 * (size_t)n);
@@ -543,6 +547,7 @@ int build_family(int family, const cwbl_var_params *vp, std::vector<TreeDesc> &d
       }
       auto nt = std::make_unique<TreeBufs>();
       nt->entry = pd.entry; nt->dim = tdim; nt->hinv = pd.hinv; nt->vinv = pd.vinv;
+      nt->bin_div_opt = S.bin_div;
       build_kdtree(nx.data(), n, tdim, nt->host);
       nt->depth = tree_depth(nt->host);
       if (nt->depth >= kSearchStackDepth)
@@ -788,6 +793,7 @@ int cwbl_init(const cwbl_init_params *p) {
   select_kp();
   S.max_batch = 160000;
   S.max_batch_set = false;
+  S.info_window = 1LL << 25;
   S.inited = true;
   return CWBL_OK;
 }
@@ -822,7 +828,7 @@ int cwbl_set_option(int option, long long value) {
       return CWBL_OK;
     case CWBL_OPT_BIG_PATH:
       if (!range(0, 2)) break;
-      S.big_split = value == 1;
+      S.big_split = value >= 1;  // (2 at k <= 96: the hand-off path, as 1)
       S.band = value == 2;
       return CWBL_OK;
     case CWBL_OPT_BIG_BATCH:
@@ -845,6 +851,10 @@ int cwbl_set_option(int option, long long value) {
       if (value != 0 && !range(256, 1LL << 31)) break;
       S.max_batch = value ? value : 160000;
       S.max_batch_set = value != 0;  // an explicit cap is used as given
+      return CWBL_OK;
+    case CWBL_OPT_INFO_WINDOW:
+      if (value != 0 && !range(256, 1LL << 30)) break;
+      S.info_window = value ? value : (1LL << 25);
       return CWBL_OK;
     default:
       return fail(CWBL_ERR_ARG, "cwbl_set_option: unknown option %d", option);
@@ -1213,12 +1223,11 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   int nrec = 0;                 // record batches so far
   std::vector<int> rec_done;    // cevent after each record batch's solve (on S.tstream)
   std::vector<int> info_done;   // cevent after each search batch's info reduction
-  // one-stream path: the info of a window of up to kInfoWindow points (the whole call below
-  // that), reduced once per window (a reduction kernel per batch cost the C2 step ~0.5 ms);
-  // the two-stream record path alternates two batch-sized buffers, reduced per batch
-  constexpr long long kInfoWindow = 1LL << 25;  // 256 MB of int2
+  // one-stream path: the info of a window of up to S.info_window points (the whole call
+  // below that), reduced once per window; the two-stream record path alternates two
+  // batch-sized buffers, reduced per batch
   const long long info_cap =
-      conc ? B : std::max<long long>(B, std::min<long long>(npts, kInfoWindow));
+      conc ? B : std::max<long long>(B, std::min<long long>(npts, S.info_window));
   HIPCHK(S.info.ensure((size_t)info_cap * sizeof(int2)));
   if (conc) HIPCHK(S.info2.ensure((size_t)B * sizeof(int2)));
   long long win0 = 0;  // first point of the current info window (one stream)

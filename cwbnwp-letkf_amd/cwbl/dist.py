@@ -30,7 +30,8 @@ def shard_columns(nx, ny, rank, world):
 #     radar: xyz (n,3) | obs (n,) | hdxb (k,n)
 # The reference sends these as ~8 ibcasts and 2 iallgatherv per GTS type and 5 ibcasts + 1
 # iallgatherv per radar type, after an mpi_bcast of the counts; here the counts ride in the
-# header and the whole set is one message (preceded by its length).
+# header and the whole set is one message (one broadcast when every rank knows the layout,
+# else preceded by its length).
 WIRE_MAGIC = 0x4C4B4631  # "LKF1"
 
 
@@ -117,22 +118,52 @@ def builder_from(types, memory):
     return b
 
 
-def broadcast_obs_set(types, k, device, src=0, group=None):
+def wire_layout(types):
+    """The header of a set as (family, type_id, nvar, nobs) per type: what every rank must know
+    to size the receive buffer of a one-collective broadcast (the reference broadcasts the
+    same counts ahead of the data, module_gts_omboma.f90:524-531)."""
+    out = []
+    for t in types:
+        fam = int(t["family"])
+        n = int(np.asarray(t["xyz"]).shape[0]) if "nobs" not in t else int(t["nobs"])
+        nvar = (int(t["nvar"]) if "nvar" in t else int(np.asarray(t["obs"]).shape[1])) \
+            if fam == 0 else 1
+        out.append((fam, int(t["type_id"]), nvar, n))
+    return out
+
+
+def wire_words(layout, k):
+    """Length in words of the wire buffer of a set with this layout."""
+    return 3 + 4 * len(layout) + sum(_type_words(f, nv, n, k) for f, _, nv, n in layout)
+
+
+def broadcast_obs_set(types, k, device, src=0, group=None, layout=None):
     """The obs-set exchange of a cycle: `src` packs its set (`types`, ignored elsewhere),
-    every rank receives it into one buffer on `device`.  Two broadcasts: the 8-byte length,
-    then the set.  Returns (k, types) as views into the received buffer."""
+    every rank receives it into one buffer on `device`.  Returns (k, types) as views into the
+    received buffer.
+
+    With `layout` (wire_layout of the set, known to every rank: the counts the reference
+    broadcasts ahead of its data) the exchange is ONE broadcast of the whole set, sized from
+    the layout.  Without it the length goes first (one 8-byte broadcast), then the set."""
     import torch
     import torch.distributed as dist
     rank = dist.get_rank(group)
+    gsrc = src if group is None else dist.get_global_rank(group, src)
     if rank == src:
         buf = torch.from_numpy(pack_obs_set(types, k)).to(device)
-        ln = torch.tensor([buf.shape[0]], dtype=torch.int64, device=device)
+        if layout is not None and (wire_layout(types) != [tuple(x) for x in layout]
+                                   or buf.shape[0] != wire_words(layout, k)):
+            raise ValueError("broadcast_obs_set: the set does not match the agreed layout")
+    if layout is not None:
+        if rank != src:
+            buf = torch.empty(wire_words(layout, k), dtype=torch.float32, device=device)
     else:
-        ln = torch.zeros(1, dtype=torch.int64, device=device)
-    dist.broadcast(ln, src=src, group=group)
-    if rank != src:
-        buf = torch.empty(int(ln.item()), dtype=torch.float32, device=device)
-    dist.broadcast(buf, src=src, group=group)
+        ln = torch.tensor([buf.shape[0] if rank == src else 0], dtype=torch.int64,
+                          device=device)
+        dist.broadcast(ln, src=gsrc, group=group)
+        if rank != src:
+            buf = torch.empty(int(ln.item()), dtype=torch.float32, device=device)
+    dist.broadcast(buf, src=gsrc, group=group)
     return unpack_obs_set(buf)
 
 

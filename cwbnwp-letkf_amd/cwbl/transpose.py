@@ -79,13 +79,18 @@ class Decomposition:
 
 
 class Transposer:
-    """One rank's side of the transposes.  `core` is the cwbl.abi.Core of this process."""
+    """One rank's side of the transposes.  `core` is the cwbl.abi.Core of this process.
 
-    def __init__(self, core, k, nx, ny, group=None, device=None):
+    `loopback`: every chunk goes through the transport, a rank's own chunk included (a send
+    to itself), and write_mean's reduce runs at world 1 too.  Off, a rank copies its own
+    chunk and a one-rank job never communicates; on, a one-GPU RCCL job executes every
+    collective and point-to-point call of the multi-GPU path (tests/test_gpu_rccl.py)."""
+
+    def __init__(self, core, k, nx, ny, group=None, device=None, loopback=False):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
-        self.core, self.k, self.group = core, k, group
+        self.core, self.k, self.group, self.loopback = core, k, group, bool(loopback)
         if dist.is_available() and dist.is_initialized():
             self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
             self.backend = dist.get_backend(group)
@@ -120,7 +125,16 @@ class Transposer:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
             return
-        # gloo (tests): host staging, one tag per message
+        # gloo (tests): host staging, one tag per message; gloo has no pair to the rank
+        # itself, so loopback messages are matched in posting order and copied
+        own_s = [t for p, _, t in sends if p == self.rank]
+        own_r = [t for p, _, t in recvs if p == self.rank]
+        if len(own_s) != len(own_r):
+            raise RuntimeError("transpose: unmatched loopback messages")
+        for a, b in zip(own_s, own_r):
+            b.copy_(a)
+        sends = [x for x in sends if x[0] != self.rank]
+        recvs = [x for x in recvs if x[0] != self.rank]
         reqs, landing = [], []
         for p, tag, t in sends:
             h = t.cpu()
@@ -171,7 +185,7 @@ class Transposer:
             self._member_sum(packed, n, len(mine), total)
         else:
             total.zero_()
-        if self.world > 1:
+        if self.world > 1 or (self.loopback and self.backend is not None):
             if self.backend == "nccl":
                 dist.reduce(total, dst=self._peer(root), op=dist.ReduceOp.SUM, group=self.group)
             else:  # gloo (tests): host staging
@@ -277,7 +291,7 @@ class Transposer:
         lx, ly = self.local_shape(stagger)
         mine = self.owned()
         n = gx * gy * nz
-        if self.world == 1 and out is None:
+        if self.world == 1 and out is None and not self.loopback:
             st = self._stacked([fields[m] for m in mine], (nz, gy, gx))
             if st is not None and st[1] == n:
                 base = st[0]
@@ -286,7 +300,7 @@ class Transposer:
                                                        device=self.device)
         chunks = self.dec.chunks(nz, stagger)
         self._sync()
-        if self.world == 1:  # the one chunk is this rank's slab: pack straight into it
+        if self.world == 1 and not self.loopback:  # the one chunk is this rank's slab
             self._pack([fields[m] for m in mine], gx, gy, nz, var, lx * ly * nz)
             self._sync()
             return var
@@ -299,11 +313,11 @@ class Transposer:
             if src == self.rank:
                 i = mine.index(m)
                 for d, (off, cnt) in enumerate(chunks):
-                    if d == self.rank:
+                    if d == self.rank and not self.loopback:
                         var[m].view(-1).copy_(packed[i, off:off + cnt])
                     elif cnt:
                         sends.append((d, m, packed[i, off:off + cnt]))
-            elif lx * ly * nz:
+            if (src != self.rank or self.loopback) and lx * ly * nz:
                 recvs.append((src, m, var[m].view(-1)))
         self._sync()
         self._exchange(sends, recvs)
@@ -322,7 +336,9 @@ class Transposer:
         chunks = self.dec.chunks(nz, stagger)
         mine = self.owned()
         out = out if out is not None else {}
-        if self.world == 1:
+        if self.world == 1 and not self.loopback:
+            if not var.is_contiguous() or var.dtype != torch.float32:
+                raise ValueError("gather_grid: var must be a contiguous float32 slab")
             todo = [m for m in mine
                     if out.get(m) is not None and out[m].data_ptr() != var[m].data_ptr()]
             for m in mine:
@@ -344,11 +360,11 @@ class Transposer:
             if dst == self.rank:
                 buf = bufs[mine.index(m)]
                 for s, (off, cnt) in enumerate(chunks):
-                    if s == self.rank:
+                    if s == self.rank and not self.loopback:
                         buf[off:off + cnt].copy_(var[m].reshape(-1))
                     elif cnt:
                         recvs.append((s, m, buf[off:off + cnt]))
-            elif var[m].numel():
+            if (dst != self.rank or self.loopback) and var[m].numel():
                 sends.append((dst, m, var[m].reshape(-1).contiguous()))
         self._exchange(sends, recvs)
         self._sync()
@@ -377,11 +393,11 @@ class Transposer:
             self.core.pack_columns(field, gx, gy, nz, self.dec.px, self.dec.py, packed)
             keep.append(packed)
             for d, (off, cnt) in enumerate(chunks):
-                if d == root:
+                if d == root and not self.loopback:
                     local.view(-1).copy_(packed[off:off + cnt])
                 elif cnt:
                     sends.append((d, 0, packed[off:off + cnt]))
-        elif local.numel():
+        if (self.rank != root or self.loopback) and local.numel():
             recvs.append((root, 0, local.view(-1)))
         self._exchange(sends, recvs)
         self._sync()

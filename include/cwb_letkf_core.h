@@ -300,14 +300,19 @@ enum {
   CWBL_OPT_SEARCH = 5,         /* 0 uniform bins + tree for truncated lists (default); 1 the
                                 * k-d tree walk for every point */
   CWBL_OPT_BIG_PATH = 6,       /* k = 65..128: 1 256-thread hand-off + one-wave tail (default);
-                                * 0 one 256-thread kernel; 2 (k = 97..128) two-stage: band
-                                * reduction on the matrix cores + one-wave bulge chase */
+                                * 0 one 256-thread kernel; 2 two-stage at k = 97..128 (band
+                                * reduction on the matrix cores + one-wave bulge chase), the
+                                * hand-off path at k = 65..96 as with 1 */
   CWBL_OPT_BIG_BATCH = 7,      /* points per k > 64 sub-batch (>= 64; default 98 304) */
   CWBL_OPT_PAGEABLE = 8,       /* pageable host slab: 0 page-lock in place (default); 1 bounce
                                 * through the library's page-locked slots */
-  CWBL_OPT_BIN_DIV = 9,        /* search bin side = radius / value, 1..8 (0 = by obs density) */
+  CWBL_OPT_BIN_DIV = 9,        /* search bin side = radius / value, 1..8 (0 = by obs density);
+                                * applies to the next cwbl_analyze_var (cached bins of another
+                                * divisor are rebuilt) */
   CWBL_OPT_LEAD_DIV = 10,      /* first search batch = points / value (0 = off, default) */
-  CWBL_OPT_MAX_BATCH = 11      /* points per search batch, >= 256 (0 = automatic, default) */
+  CWBL_OPT_MAX_BATCH = 11,     /* points per search batch, >= 256 (0 = automatic, default) */
+  CWBL_OPT_INFO_WINDOW = 12    /* points per reduction of the per-point solve info, >= 256
+                                * (0 = 2^25, default; smaller values exercise the rollover) */
 };
 int         cwbl_set_option(int option, long long value);
 

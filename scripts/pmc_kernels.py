@@ -77,6 +77,7 @@ def main(src, tag):
                 if "fp64_flops_per_launch" in e and e["points_per_launch"]:
                     e["fp64_flops_per_point"] = e["fp64_flops_per_launch"] / e["points_per_launch"]
             out[k] = e
+        out["_meta"] = {"steps": 1}  # profile_round.sh profiles one step (--steps 1 --warmup 0)
         pm["configs"][cfg] = out
         os.makedirs("profiles", exist_ok=True)
         shutil.copy(ks, f"profiles/{tag}_{cfg}_kernel_stats.csv")

@@ -707,6 +707,31 @@ def test_band_path_vs_one_kernel_and_oracle(k, sparse):
     assert rel <= INCR_TOL, rel
 
 
+def test_info_window_rollover_matches_single_window():
+    """The per-point solve info (solved flag, p) is reduced once per window of
+    CWBL_OPT_INFO_WINDOW points (2^25 by default, so one window below 33.5 M points).  Small
+    windows over small search batches force many rollovers (the g0 - win0 offsets, a window
+    closing mid-call): the statistics and the analysis must equal the one-window run's."""
+    from cwbl import synth
+    w = synth.make("c2", seed=23, scale=0.1, nz=10)  # 30 x 30 x 10 = 9 000 points, k = 40
+    runs = []
+    for opts in ({}, {"max_batch": 256, "info_window": 256},
+                 {"max_batch": 1000, "info_window": 2500}, {"info_window": 4096}):
+        _cores.clear()
+        c = abi.Core(w.k, device=0, options=opts)
+        c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+        var = w.var.copy()
+        st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+        c.finalize()
+        runs.append((var, (st.points, st.solved, st.nobs_sum, st.max_p, st.lz_truncated,
+                           st.nonconverged)))
+    _cores.clear()
+    assert runs[0][1][1] > 0
+    for var, stats in runs[1:]:
+        assert stats == runs[0][1]
+        np.testing.assert_array_equal(var.view(np.uint32), runs[0][0].view(np.uint32))
+
+
 def test_tune_q_matches_reference():
     """letkf_tune_q on the device (cwbl_var_params.tune_q) against the reference's compiled
     letkf_tune_q (G5): bit for bit, including the Q3 NaN columns.  The single obs lies far

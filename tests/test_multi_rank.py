@@ -82,7 +82,7 @@ def _wire_types(case):
     return out
 
 
-def _worker_obs_set(rank, world, port, out_dir):
+def _worker_obs_set(rank, world, port, out_dir, with_layout=False):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(repo, "tests"))
@@ -91,7 +91,16 @@ def _worker_obs_set(rank, world, port, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     case = DriverCase("driver_mixed.npz")
     types = _wire_types(case) if rank == 0 else None
-    k, got = cdist.broadcast_obs_set(types, case.k, torch.device("cpu"), src=0)
+    layout = cdist.wire_layout(_wire_types(case)) if with_layout else None
+    calls = []
+    real = dist.broadcast
+    dist.broadcast = lambda *a, **kw: (calls.append(1), real(*a, **kw))[1]
+    try:
+        k, got = cdist.broadcast_obs_set(types, case.k, torch.device("cpu"), src=0,
+                                         layout=layout)
+    finally:
+        dist.broadcast = real
+    assert len(calls) == (1 if with_layout else 2), calls
     got = [{key: (v.numpy() if isinstance(v, torch.Tensor) else v) for key, v in t.items()}
            for t in got]
     ob = cdist.builder_from(got, abi.MEM_HOST).build()
@@ -104,16 +113,18 @@ def _worker_obs_set(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_obs_set_broadcast_carries_the_whole_set(tmp_path):
+@pytest.mark.parametrize("with_layout", [False, True])
+def test_obs_set_broadcast_carries_the_whole_set(tmp_path, with_layout):
     """The obs-set wire format (GTS sound/synop/metar with QC + radar dbz/vr) through the
     broadcast of a 2-rank gloo group: every rank's analysis of the received set equals the
-    reference's output for the G4 mixed case bit for bit."""
+    reference's output for the G4 mixed case bit for bit.  With the layout (the counts every
+    rank knows) the exchange is ONE broadcast; without it the length goes first."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from helpers import DriverCase
     world = 2
-    mp.spawn(_worker_obs_set, args=(world, _free_port(), str(tmp_path)), nprocs=world,
-             join=True)
+    mp.spawn(_worker_obs_set, args=(world, _free_port(), str(tmp_path), with_layout),
+             nprocs=world, join=True)
     ref = DriverCase("driver_mixed.npz").var_out
     for r in range(world):
         got = np.load(tmp_path / f"obs_rank{r}.npy")
@@ -142,6 +153,21 @@ def test_obs_set_wire_roundtrip():
     bad[0] = 0.0
     with pytest.raises(ValueError):
         cdist.unpack_obs_set(bad)
+
+
+def test_wire_layout_sizes_the_buffer():
+    """wire_words(wire_layout(set)) is the packed length, for raw and unpacked types; a set
+    that does not match the agreed layout is refused before anything is sent."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from helpers import DriverCase
+    case = DriverCase("driver_mixed.npz")
+    types = _wire_types(case)
+    buf = cdist.pack_obs_set(types, case.k)
+    lay = cdist.wire_layout(types)
+    assert cdist.wire_words(lay, case.k) == buf.shape[0]
+    assert cdist.wire_layout(cdist.unpack_obs_set(buf)[1]) == lay
+    assert {f for f, _, _, _ in lay} == {0, 1}
 
 
 def test_shard_columns_partition():

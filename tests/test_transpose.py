@@ -168,20 +168,23 @@ def check_plan(out_dir, world, k, nx, ny, nz):
         np.testing.assert_array_equal(res[r]["lon"], lon[r][0, 0])
 
 
-def _worker(rank, world, port, out_dir, k, nx, ny, nz):
+def _worker(rank, world, port, out_dir, k, nx, ny, nz, loopback=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    t = tr.Transposer(OracleCore(), k, nx, ny, device=torch.device("cpu"))
+    t = tr.Transposer(OracleCore(), k, nx, ny, device=torch.device("cpu"), loopback=loopback)
     run_plan(t, k, nx, ny, nz, out_dir, rank)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k", [(2, 5), (3, 4)])
-def test_transposes_gloo(tmp_path, world, k):
+@pytest.mark.parametrize("world,k,loopback", [(2, 5, False), (3, 4, False), (1, 3, True),
+                                              (2, 5, True)])
+def test_transposes_gloo(tmp_path, world, k, loopback):
+    """The whole plan over gloo ranks against the oracle.  loopback: a rank's own chunk goes
+    through the transport too (the one-GPU RCCL exercise, tests/test_gpu_rccl.py)."""
     nx, ny, nz = 7, 5, 3
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), k, nx, ny, nz), nprocs=world,
-             join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), k, nx, ny, nz, loopback),
+             nprocs=world, join=True)
     check_plan(str(tmp_path), world, k, nx, ny, nz)
 
 
