@@ -11,10 +11,11 @@ cwbl_pack_columns / cwbl_unpack_columns / cwbl_vcoord_mean kernels.
                      BLAS order in fp32 (y = 0; y += (alpha*1)*A(:,j)), and the same call
                      through MKL's sgemv_ (what an MKL-linked reference computes)
 
-module_mpi_util itself cannot be compiled here (it needs an MPI Fortran module, which this
-image lacks for amdflang), so the scatter/gather restatement is checked by its own
-invariants (every element lands exactly once, gather inverts scatter) and against the index
-arithmetic of the loops it cites; the mean is pinned by MKL's sgemv_.
+Pinned bit for bit against the reference itself: oracle/ref/build_mpi_util.sh compiles
+module_mpi_util.f90 from /root/reference (MPICH's mpif.h behind a `module mpi` wrapper, the
+image's mpi.mod being gfortran's), oracle/gen_mpi_util_goldens.py runs it under mpirun at
+2, 6 and 8 ranks, and tests/test_mpi_util_golden.py checks every function below against
+every rank's output (tests/golden/mpi_util_n*_k*.npz).
 Arrays: a global field is global(nx,ny,nz) Fortran order = numpy (nz,ny,nx) C order; a local
 slab var(loc_nx,loc_ny,nz,0:k-1) = numpy (k,nz,loc_ny,loc_nx).
 """

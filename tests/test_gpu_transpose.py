@@ -209,3 +209,42 @@ def test_write_mean_single_rank():
             acc = acc + allf[m][i]
         np.testing.assert_array_equal(out[i].cpu().numpy().view(np.uint32),
                                       (inv * acc).view(np.uint32))
+
+
+# ---- the kernels against the reference's own module_mpi_util (tests/golden/mpi_util_*.npz) --
+from test_mpi_util_golden import FIXTURES, load  # noqa: E402
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_pack_unpack_vcoord_kernels_vs_reference_fixtures(path):
+    """cwbl_pack_members / cwbl_unpack_members / cwbl_vcoord_mean on the inputs the compiled
+    reference's letkf_scatter_grid / letkf_gather_grid / letkf_scatter_vcoord saw under
+    mpirun: a member's packed buffer is the ranks' slabs in rank order (the alltoallv
+    sdispls), unpacking the ranks' 2 * var gives the reference's gathered members, and the
+    vertical coordinate of every rank equals its sgemv mean (MKL) bit for bit."""
+    g, nproc, k, nx, ny, nz = load(path)
+    c = core(max(k, 2))
+    px, py = tr.dims_create(nproc)
+    for st in (0, 1, 2):
+        gx, gy = nx + (st == 1), ny + (st == 2)
+        n = gx * gy * nz
+        members = torch.from_numpy(np.stack([g[f"r{m}_s{st}_in"] for m in range(k)])).cuda()
+        send = torch.full((k * n,), float("nan"), device="cuda")
+        c.pack_members(members, n, k, gx, gy, nz, px, py, send, n)
+        want = np.stack([np.concatenate([g[f"r{r}_s{st}_local"][m].ravel() for r in range(nproc)])
+                         for m in range(k)])
+        np.testing.assert_array_equal(send.cpu().numpy().reshape(k, n), want)
+        recv = torch.from_numpy(np.float32(2.0) * want).cuda()
+        out = torch.full((k, nz, gy, gx), float("nan"), device="cuda")
+        c.unpack_members(recv, n, k, gx, gy, nz, px, py, out, n)
+        got = out.cpu().numpy()
+        for m in range(k):
+            np.testing.assert_array_equal(got[m], g[f"r{m}_s{st}_back"])
+    for tag, stagger, nzp in (("v0", 0, nz + 1), ("v1", 1, nz)):
+        tmp4d = mo.scatter_grid([g[f"r{m}_{tag}_in"] for m in range(k)], nproc, 0)
+        for r in range(nproc):
+            lx, ly = int(g[f"r{r}_info"][0]), int(g[f"r{r}_info"][1])
+            alt = torch.empty((nz, ly, lx), device="cuda")
+            c.vcoord_mean(torch.from_numpy(tmp4d[r]).cuda(), lx * ly, nzp, k, stagger, tr.G, alt)
+            np.testing.assert_array_equal(alt.cpu().numpy().view(np.uint32),
+                                          g[f"r{r}_{tag}_out"].view(np.uint32))
