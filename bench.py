@@ -514,13 +514,6 @@ def kernel_algorithmic_flops(name, k, solved, nobs_sum):
         return solved * _tri_flops(k, j0, k) + vec
     if name.startswith("solve_tq_kernel") or name.startswith("solve_tq_big_kernel"):
         return syrk + solved * _tri_flops(k, 0, k) + vec
-    # two-stage band path: the head does the O(k^3) part of the reduction (priced as dsytd2's
-    # count, which the band reduction's panels and trailing updates replace); the chase is
-    # O(b k^2) work dsytd2 does not have, so the tail is credited the vector work only
-    if name.startswith("band_head_kernel"):
-        return syrk + solved * _tri_flops(k, 0, k)
-    if name.startswith("band_tail_kernel"):
-        return vec
     if name.startswith("solve_kernel"):  # Jacobi: the eigendecomposition itself
         return synth.flops_total(k, solved, nobs_sum)
     return None
@@ -675,9 +668,9 @@ def main():
                     help="skip the wall-clock-per-cycle detail (16 var_update entries)")
     ap.add_argument("--no-detail-configs", action="store_true",
                     help="skip the C4 / C5 / host-memory detail legs")
-    ap.add_argument("--big-path", type=int, choices=(0, 1, 2), default=None,
+    ap.add_argument("--big-path", type=int, choices=(0, 1), default=None,
                     help="CWBL_OPT_BIG_PATH for k > 64 (default: the library's, 1 = hand-off; "
-                         "2 = the two-stage band path at k > 96)")
+                         "0 = one 256-thread kernel)")
     args = ap.parse_args()
     if args.big_path is not None:
         CORE_OPTIONS["big_path"] = args.big_path

@@ -205,7 +205,7 @@ struct TreeBufs {
 enum KernelId {
   KT_SEARCH_BINNED, KT_SEARCH_FLAGGED, KT_SEARCH_TREE, KT_ASSEMBLE_RECORD, KT_SOLVE_TQ40,
   KT_BIG_HANDOFF, KT_TQB_TAIL, KT_SOLVE_TQ, KT_SOLVE_TQ_BIG, KT_SOLVE_JACOBI, KT_TUNE_Q,
-  KT_BAND_HEAD, KT_BAND_TAIL, KT_COUNT
+  KT_COUNT
 };
 struct KTime { long long launches = 0, points = 0; double ms = 0.0; };
 
@@ -222,10 +222,7 @@ struct State {
   DevBuf tdesc, nbr_cnt, nbr_idx, info, stats;
   DevBuf nbr_cnt2, nbr_idx2;                          // second list buffer (search overlap)
   hipStream_t sstream = nullptr;                      // neighbour searches of later batches
-  hipStream_t tstream = nullptr;                      // solve_tq40_kernel (record path)
-  bool tq40_streams = false;  // CWBL_OPT_SPLIT40_STREAMS: solve_tq40_kernel on its own stream
-  DevBuf wsa2, info2;                                 // second record / info buffers
-  std::vector<hipEvent_t> cevents;                    // record-path events (cevent)
+  std::vector<hipEvent_t> cevents;                    // ordering events of the host copies
   int lead_div = 0;                                   // first batch = npts / lead_div (0: off)
   bool serial_search = false;                         // CWBL_DEBUG_SERIAL=1: searches on S.stream
   // Points per search/solve batch.  Measured on C2 (one GPU, ms per variable): 40 k 113,
@@ -251,7 +248,6 @@ struct State {
   int tq4 = 1;  // CWBL_OPT_SPLIT40: KP=40 solve 0 = one kernel, else assembly record + solve_tq40
   long long tq4_sub = 0;                              // CWBL_TQ4_SUB: record batch (points)
   bool big_split = true;                              // big_path 1: hand-off + one-wave tail
-  bool band = false;                                  // big_path 2 (KP = 128): two-stage band path
   long long big_sub = 98304;                          // CWBL_OPT_BIG_BATCH: k > 64 sub-batch
   std::vector<hipEvent_t> events;
   hipStream_t h2d = nullptr, d2h = nullptr;           // host-memory slab copies (pipelined)
@@ -312,7 +308,7 @@ hipError_t stage(DevBuf &dst, const void *src, size_t bytes, int memory) {
                         S.stream);
 }
 
-hipError_t cevent(int i, hipEvent_t *out) {  // events of the record path (timing off)
+hipError_t cevent(int i, hipEvent_t *out) {  // ordering events (timing off)
   while ((int)S.cevents.size() <= i) {
     hipEvent_t e;
     hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -425,8 +421,6 @@ std::string kernel_name(int id) {
     case KT_SOLVE_TQ_BIG: return "solve_tq_big_kernel<" + kp + ", false>";
     case KT_SOLVE_JACOBI: return "solve_kernel<" + kp + ", false>";
     case KT_TUNE_Q: return "tune_q_kernel";
-    case KT_BAND_HEAD: return "band_head_kernel<false>";
-    case KT_BAND_TAIL: return "band_tail_kernel";
   }
   return "?";
 }
@@ -633,11 +627,8 @@ void release_obs() {
 
 void release_all() {
   release_obs();
-  for (DevBuf *b : {&S.wsa2, &S.info2}) b->release();
   for (hipEvent_t e : S.cevents) (void)hipEventDestroy(e);
   S.cevents.clear();
-  if (S.tstream) (void)hipStreamDestroy(S.tstream);
-  S.tstream = nullptr;
   for (DevBuf *b : {&S.tdesc, &S.nbr_cnt, &S.nbr_idx, &S.nbr_cnt2, &S.nbr_idx2, &S.info, &S.stats, &S.sx,
                     &S.sy, &S.salt, &S.svar, &S.bcol, &S.byo, &S.byb, &S.bxb, &S.bxa, &S.bev, &S.btri,
                     &S.qxyz, &S.qnf, &S.qidx, &S.qr2, &S.quad, &S.wsa, &S.flags})
@@ -701,6 +692,463 @@ SolveConsts solve_consts(float inflat, int use_rtpp, float rtpp_a, int use_rtps,
   return c;
 }
 
+// ---- cwbl_analyze_var by stage ---------------------------------------------------------------
+// One call of cwbl_analyze_var (letkf_driver's per-variable body, module_letkf_core.f90:59-297):
+//   plan_trees      build_tree x2 (cached per obs set) + the QC column tables   (:63-64)
+//   stage_slab      the slab in device memory (host slabs staged / piped)
+//   plan_batches    search/solve batches
+//   per batch       search_batch (S.sstream) -> solve_batch_path (S.stream), with the host
+//                   slab's var piped in and out around it (S.h2d / S.d2h)        (:209-240)
+//   finish_call     info reduction, tune_q (:253-278), write-back, statistics
+struct VarCall {
+  const cwbl_var_params *vp = nullptr;
+  const cwbl_slab *sl = nullptr;
+  long long npts = 0, L = 0;
+  SlabDev sd{};
+  size_t bvar = 0;
+  // host-memory slab: x, y, alt staged first; var piped batch by batch (piped: the analysed
+  // region is the whole horizontal slab, so a batch's points are contiguous in every member
+  // plane) or moved whole; a pageable var page-locked in place (registered) or, failing that,
+  // through the library's page-locked bounce slots
+  bool host = false, piped = false, piped_back = false, bounce = false, registered = false;
+  std::vector<TreeDesc> descs;
+  int list_cap = 0, max_depth = 1, nt = 0;
+  std::vector<std::pair<long long, int>> plan;  // (g0, nb)
+  long long B = 0, Bc = 0, info_cap = 0, win0 = 0;
+  SolveConsts c{};
+  float rbox = 0.0f;
+  // timing events S.events[ev..] (four per batch: search begin/end, solve begin/end) and
+  // ordering events S.cevents[cev..] of the piped copies
+  int ev = 4, cev = 0;
+  std::vector<std::pair<int, int>> search_ev, solve_ev;
+  std::vector<int> done_ev, h2d_done, d2h_done;
+};
+
+// build_tree of both families and the upload of their descriptors (nt = 0: nothing to do)
+int plan_trees(VarCall &v) {
+  if (int rc = build_family(0, v.vp, v.descs, v.list_cap, v.max_depth)) return rc;
+  if (int rc = build_family(1, v.vp, v.descs, v.list_cap, v.max_depth)) return rc;
+  v.nt = (int)v.descs.size();
+  if (v.nt == 0 || v.npts == 0) return CWBL_OK;
+  HIPCHK(S.tdesc.ensure(v.descs.size() * sizeof(TreeDesc)));
+  HIPCHK(hipMemcpyAsync(S.tdesc.p, v.descs.data(), v.descs.size() * sizeof(TreeDesc),
+                        hipMemcpyHostToDevice, S.stream));
+  return CWBL_OK;
+}
+
+int stage_slab(VarCall &v) {
+  const cwbl_slab *sl = v.sl;
+  v.L = (long long)sl->nx * sl->ny * sl->nz;
+  SlabDev &sd = v.sd;
+  sd.nx = sl->nx; sd.ny = sl->ny; sd.nz = sl->nz; sd.alt_nx = sl->alt_nx;
+  sd.alt_ny = sl->alt_ny; sd.ix_lim = sl->ix_lim; sd.iy_lim = sl->iy_lim; sd.L = v.L;
+  const size_t bxy = (size_t)sl->nx * sl->ny * 4;
+  const size_t balt = (size_t)sl->alt_nx * sl->alt_ny * sl->nz * 4;
+  v.bvar = (size_t)v.L * S.k * 4;
+  v.host = sl->memory != CWBL_MEM_DEVICE;
+  v.piped = v.host && sl->ix_lim == sl->nx && sl->iy_lim == sl->ny;
+  v.piped_back = v.piped && !v.vp->tune_q;  // tune_q touches the whole slab afterwards
+  // pageable var (a Fortran host's ordinary arrays): copies from pageable memory are staged by
+  // the runtime and do not overlap.  It is page-locked in place for the call (r4, C2 from
+  // pageable numpy arrays: 58.7 M pts/s, against 58.2 M page-locked and 50.8 M through the
+  // bounce slots, whose host copies stall the pipeline); the slots remain the fallback when
+  // the registration fails (and CWBL_OPT_PAGEABLE = 1 forces them)
+  v.bounce = v.host && v.bvar > 0 && !host_pinned(sl->var);
+  if (v.bounce && S.pageable_register) {
+    if (hipHostRegister(sl->var, v.bvar, hipHostRegisterDefault) == hipSuccess) {
+      v.registered = true;
+      v.bounce = false;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
+  if (!v.host) {
+    sd.x = sl->x; sd.y = sl->y; sd.alt = sl->alt; sd.var = sl->var;
+    return CWBL_OK;
+  }
+  HIPCHK(stage(S.sx, sl->x, bxy, CWBL_MEM_HOST));
+  HIPCHK(stage(S.sy, sl->y, bxy, CWBL_MEM_HOST));
+  HIPCHK(stage(S.salt, sl->alt, balt, CWBL_MEM_HOST));
+  if (v.piped || v.bounce) HIPCHK(S.svar.ensure(v.bvar));
+  else HIPCHK(stage(S.svar, sl->var, v.bvar, CWBL_MEM_HOST));
+  sd.x = S.sx.as<float>(); sd.y = S.sy.as<float>(); sd.alt = S.salt.as<float>();
+  sd.var = S.svar.as<float>();
+  return CWBL_OK;
+}
+
+void plan_batches(VarCall &v) {
+  const long long npts = v.npts;
+  const size_t per_pt = (size_t)v.list_cap * 4 + (size_t)v.nt * 4 + 8;
+  long long B = (long long)(S.ws_bytes / per_pt);
+  B = std::min<long long>(B, S.max_batch);
+  // at least ~6 batches while they stay above 64 k points: with few batches the first search
+  // and the last solve run alone (an 8-GPU rank's C2 share, 562 k points: 12.8 ms per step
+  // in batches of 141 k, 12.3 in batches of 94 k; the full grid is indifferent in 100-160 k)
+  if (!S.max_batch_set) B = std::min<long long>(B, std::max<long long>(npts / 6, 64000));
+  B = std::max<long long>(std::min<long long>(B, npts), 256);
+  B = std::min<long long>(B, 1 << 22);
+  // a batch's lists stay below 4 GiB: search_binned_kernel addresses them by 32-bit offsets
+  if (v.list_cap > 0)
+    B = std::min<long long>(B, (long long)((((size_t)1 << 32) - 1) / ((size_t)v.list_cap * 4)) /
+                                   kListLanes * kListLanes);
+  // The first batch's search cannot overlap a solve, so it may be short (a lead of
+  // 1/lead_div of the points); the rest are equal (a short last batch is all tail) and whole
+  // list groups.
+  const auto round_up = [](long long x) { return (x + kListLanes - 1) / kListLanes * kListLanes; };
+  long long lead = S.lead_div > 0 ? round_up(npts / S.lead_div) : 0;
+  if (lead < 4 * kListLanes || lead >= npts) lead = 0;
+  if (lead > 0) v.plan.push_back({0, (int)std::min<long long>(lead, B)});
+  const long long g1 = v.plan.empty() ? 0 : v.plan[0].second, rest = npts - g1;
+  const long long nrest = (rest + B - 1) / B;
+  const long long Br = round_up((rest + nrest - 1) / nrest);
+  for (long long g = g1; g < npts; g += Br)
+    v.plan.push_back({g, (int)std::min<long long>(Br, npts - g)});
+  v.B = 0;
+  for (const auto &b : v.plan) v.B = std::max<long long>(v.B, b.second);
+  // bounce slots: one batch (or one whole-slab chunk of Bc points) of k member rows each
+  v.Bc = std::min<long long>(std::max<long long>(v.B, 1), std::max<long long>(v.L, 1));
+  // the per-point info of a window of up to S.info_window points is reduced once per window
+  // (a reduction kernel per batch cost the C2 step ~0.5 ms)
+  v.info_cap = std::max<long long>(v.B, std::min<long long>(npts, S.info_window));
+}
+
+// Whole-slab moves through the bounce slots (var not piped, or back after tune_q): chunk i of
+// Bc points of every member row.  Up: fill slot i & 1 (once its copy two chunks back has left
+// it), copy up on S.stream.  Down: copy chunk i down on S.stream, drain chunk i - 1 meanwhile.
+int bounce_whole(VarCall &v, bool up) {
+  std::vector<int> evs;
+  long long pc0 = 0;
+  int pcn = 0;
+  const size_t pitch = (size_t)v.L * 4;
+  float *const hvar = v.sl->var;
+  for (long long c0 = 0, i = 0; c0 < v.L; c0 += v.Bc, ++i) {
+    const int cn = (int)std::min<long long>(v.Bc, v.L - c0);
+    PinBuf &slot = up ? S.pin_in[i & 1] : S.pin_out[i & 1];
+    hipEvent_t e;
+    HIPCHK(cevent(v.cev, &e));
+    if (up) {
+      if (i >= 2) HIPCHK(hipEventSynchronize(S.cevents[evs[(size_t)i - 2]]));
+      bounce_rows(S.pool, slot.as<float>(), hvar, v.L, c0, cn, S.k, true);
+      HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + c0, pitch, slot.p, (size_t)cn * 4,
+                              (size_t)cn * 4, (size_t)S.k, hipMemcpyHostToDevice, S.stream));
+    } else {
+      HIPCHK(hipMemcpy2DAsync(slot.p, (size_t)cn * 4, S.svar.as<float>() + c0, pitch,
+                              (size_t)cn * 4, (size_t)S.k, hipMemcpyDeviceToHost, S.stream));
+    }
+    HIPCHK(hipEventRecord(e, S.stream));
+    evs.push_back(v.cev++);
+    if (!up && i >= 1) {
+      HIPCHK(hipEventSynchronize(S.cevents[evs[(size_t)i - 1]]));
+      bounce_rows(S.pool, S.pin_out[(i - 1) & 1].as<float>(), hvar, v.L, pc0, pcn, S.k, false);
+    }
+    pc0 = c0;
+    pcn = cn;
+  }
+  if (!up && !evs.empty()) {
+    HIPCHK(hipEventSynchronize(S.cevents[evs.back()]));
+    bounce_rows(S.pool, S.pin_out[(evs.size() - 1) & 1].as<float>(), hvar, v.L, pc0, pcn,
+                S.k, false);
+  }
+  return CWBL_OK;
+}
+
+// Piped bounce: batch b's columns into slot b % kSlots once the copy up of batch b - kSlots
+// has left it; batch b's analysis out of its slot once its copy down is done.
+int bounce_fill(VarCall &v, long long b) {
+  if (b >= State::kSlots) HIPCHK(hipEventSynchronize(S.cevents[v.h2d_done[b - State::kSlots]]));
+  bounce_rows(S.pool, S.pin_in[b % State::kSlots].as<float>(), v.sl->var, v.L, v.plan[b].first,
+              v.plan[b].second, S.k, true);
+  return CWBL_OK;
+}
+
+int bounce_drain(VarCall &v, long long b) {
+  HIPCHK(hipEventSynchronize(S.cevents[v.d2h_done[b]]));
+  bounce_rows(S.pool, S.pin_out[b % State::kSlots].as<float>(), v.sl->var, v.L, v.plan[b].first,
+              v.plan[b].second, S.k, false);
+  return CWBL_OK;
+}
+
+// The bounce slots of this call (page-locked only while a call needs them) and the whole-slab
+// move up when var is not piped.
+int stage_bounce(VarCall &v) {
+  if (v.registered) {  // the slots are only the fallback's: give them back
+    for (int i = 0; i < State::kSlots; ++i) {
+      S.pin_in[i].release();
+      S.pin_out[i].release();
+    }
+  }
+  if (!v.bounce) return CWBL_OK;
+  const size_t slot_bytes = (size_t)v.Bc * S.k * 4;
+  const int nin = v.piped ? State::kSlots : 2, nout = v.piped_back ? State::kSlots : 2;
+  for (int i = 0; i < nin; ++i) HIPCHK(S.pin_in[i].ensure(slot_bytes));
+  for (int i = 0; i < nout; ++i) HIPCHK(S.pin_out[i].ensure(slot_bytes));
+  if (!v.piped) return bounce_whole(v, true);
+  return CWBL_OK;
+}
+
+// Per-call device buffers (two neighbour-list buffers: the search of batch b + 1 overlaps the
+// solve of batch b) and the solve constants.
+int alloc_call_buffers(VarCall &v) {
+  const long long B = v.B;
+  const size_t bytes_cnt = (size_t)B * v.nt * 4;
+  const size_t bytes_idx =
+      (size_t)((B + kListLanes - 1) / kListLanes) * kListLanes * std::max(v.list_cap, 1) * 4;
+  HIPCHK(S.nbr_cnt.ensure(bytes_cnt));
+  HIPCHK(S.nbr_idx.ensure(bytes_idx));
+  if (v.plan.size() > 1) {
+    HIPCHK(S.nbr_cnt2.ensure(bytes_cnt));
+    HIPCHK(S.nbr_idx2.ensure(bytes_idx));
+  }
+  HIPCHK(S.flags.ensure((size_t)(B + 1) * sizeof(int)));
+  HIPCHK(S.stats.ensure(sizeof(DevStats)));
+  HIPCHK(hipMemsetAsync(S.stats.p, 0, sizeof(DevStats), S.stream));
+  HIPCHK(S.info.ensure((size_t)v.info_cap * sizeof(int2)));
+  v.c = solve_consts((float)(S.k - 1) / v.vp->multi_infl,  // inflat (:68)
+                     v.vp->use_rtpp, v.vp->rtpp_alpha, v.vp->use_rtps, v.vp->rtps_alpha);
+  v.c.ntrees = v.nt;
+  v.c.list_cap = v.list_cap;
+  // bounding-box half-width of the binned search: the radius with a margin, so that every
+  // point with d2 <= r2 in fp32 lies inside
+  v.rbox = std::sqrt(search_r2()) * 1.0001f + 1e-5f;
+  return CWBL_OK;
+}
+
+// get_lz for every point of batch bi (module_localization.f90:188-331) on S.sstream: uniform
+// bins, then the k-d tree walk for the points whose lists pass max_lz_pts (Q4); or the tree
+// walk for every point (CWBL_OPT_SEARCH = 1).  Waits for the solve two batches back, which
+// read the same list buffer.
+int search_batch(VarCall &v, long long bi, int *ncnt, int *nidx, hipEvent_t a, hipEvent_t b) {
+  const long long g0 = v.plan[bi].first;
+  const int nb = v.plan[bi].second;
+  const TreeDesc *dtrees = S.tdesc.as<TreeDesc>();
+  DevStats *dst = S.stats.as<DevStats>();
+  // (timing experiment: CWBL_DEBUG_SERIAL=1 runs the searches on the solve stream)
+  hipStream_t ss = S.serial_search ? S.stream : S.sstream;
+  if (bi >= 2) HIPCHK(hipStreamWaitEvent(ss, S.events[v.done_ev[bi - 2]], 0));
+  HIPCHK(hipEventRecord(a, ss));
+  int kt;
+  if (S.binned) {
+    int *fcnt = S.flags.as<int>(), *fidx = fcnt + 1;
+    HIPCHK(hipMemsetAsync(fcnt, 0, sizeof(int), ss));
+    HIPCHK(kt_begin(ss, &kt));
+    HIPCHK(launch_search_binned(ss, dtrees, v.nt, v.list_cap, v.c.r2, v.rbox, v.sd, g0, nb, ncnt,
+                                nidx, fcnt, fidx));
+    HIPCHK(kt_end(ss, kt, KT_SEARCH_BINNED, nb));
+    HIPCHK(kt_begin(ss, &kt));
+    HIPCHK(launch_search_flagged(ss, dtrees, v.nt, v.max_depth, v.list_cap, v.c.r2, v.sd, g0, nb,
+                                 fcnt, fidx, ncnt, nidx, dst));
+    HIPCHK(kt_end(ss, kt, KT_SEARCH_FLAGGED, 0));
+  } else {
+    HIPCHK(kt_begin(ss, &kt));
+    HIPCHK(launch_search(ss, dtrees, v.nt, v.max_depth, v.list_cap, v.c.r2, v.sd, g0, nb, ncnt,
+                         nidx, nullptr, dst));
+    HIPCHK(kt_end(ss, kt, KT_SEARCH_TREE, nb));
+  }
+  return hipEventRecord(b, ss) == hipSuccess ? CWBL_OK
+                                              : fail(CWBL_ERR_HIP, "search event record failed");
+}
+
+// A host slab's var columns of batch bi up (k rows of nb floats, member pitch L) on S.h2d,
+// from the caller's page-locked array or from the batch's bounce slot; S.stream waits.
+int upload_batch_var(VarCall &v, long long bi) {
+  const long long g0 = v.plan[bi].first;
+  const int nb = v.plan[bi].second;
+  hipEvent_t hv;
+  const int hv_i = v.cev++;
+  HIPCHK(cevent(hv_i, &hv));
+  const size_t pitch = (size_t)v.L * 4;
+  if (v.bounce) {  // slot bi % kSlots, filled before this batch (bounce_fill)
+    if (bi == 0)
+      if (int rc = bounce_fill(v, 0)) return rc;
+    HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + g0, pitch, S.pin_in[bi % State::kSlots].p,
+                            (size_t)nb * 4, (size_t)nb * 4, (size_t)S.k, hipMemcpyHostToDevice,
+                            S.h2d));
+  } else {
+    HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + g0, pitch, v.sl->var + g0, pitch,
+                            (size_t)nb * 4, (size_t)S.k, hipMemcpyHostToDevice, S.h2d));
+  }
+  HIPCHK(hipEventRecord(hv, S.h2d));
+  v.h2d_done.push_back(hv_i);
+  HIPCHK(hipStreamWaitEvent(S.stream, hv, 0));
+  return CWBL_OK;
+}
+
+// Batch bi's analysis back to a host slab behind its solve (event dn) on S.d2h.
+int return_batch_var(VarCall &v, long long bi, hipEvent_t dn) {
+  const long long g0 = v.plan[bi].first;
+  const int nb = v.plan[bi].second;
+  HIPCHK(hipStreamWaitEvent(S.d2h, dn, 0));
+  const size_t pitch = (size_t)v.L * 4;
+  if (v.bounce) {  // into slot bi % kSlots (drained kSlots - 1 batches later)
+    hipEvent_t dv;
+    const int dv_i = v.cev++;
+    HIPCHK(cevent(dv_i, &dv));
+    HIPCHK(hipMemcpy2DAsync(S.pin_out[bi % State::kSlots].p, (size_t)nb * 4,
+                            S.svar.as<float>() + g0, pitch, (size_t)nb * 4, (size_t)S.k,
+                            hipMemcpyDeviceToHost, S.d2h));
+    HIPCHK(hipEventRecord(dv, S.d2h));
+    v.d2h_done.push_back(dv_i);
+  } else {
+    HIPCHK(hipMemcpy2DAsync(v.sl->var + g0, pitch, S.svar.as<float>() + g0, pitch,
+                            (size_t)nb * 4, (size_t)S.k, hipMemcpyDeviceToHost, S.d2h));
+  }
+  return CWBL_OK;
+}
+
+// Sub-batches of a search batch for a path with a per-point record: ns points (a multiple of
+// kListLanes, so a sub-batch's neighbour lists start on a list group) with at most `cap`
+// points each, the batch split evenly.
+long long sub_batch(int nb, long long cap) {
+  const long long nsub = (nb + cap - 1) / cap;
+  const long long Bs = (nb + nsub - 1) / nsub;
+  return std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
+}
+
+// letkf_yoyb + letkf_solve (module_letkf_core.f90:300-700) for batch (g0, nb) on S.stream, one
+// path per ensemble-size class:
+//   k = 17..40   record path: assemble_record_kernel -> record -> solve_tq40_kernel
+//   k = 65..128  hand-off path: 256-thread kernel (assembly + first steps) -> record ->
+//                solve_tqb_tail_kernel; CWBL_OPT_BIG_PATH = 0: one 256-thread kernel
+//   otherwise    one wavefront per point: solve_tq_kernel; CWBL_OPT_SOLVER = 1: the Jacobi
+//                eigensolver kernel (k <= 64)
+// b2 / dn: the events around the batch's solve (the record path times its kernel pair
+// between them).
+int solve_batch_path(VarCall &v, long long g0, int nb, const int *ncnt, const int *nidx,
+                     int2 *infob, hipEvent_t b2, hipEvent_t dn) {
+  const TreeDesc *dtrees = S.tdesc.as<TreeDesc>();
+  const SolveConsts &c = v.c;
+  const SlabDev &sd = v.sd;
+  const int nt = v.nt, list_cap = v.list_cap;
+  int kt;
+  const bool handoff = (S.kp == 96 || S.kp == kBigSplitKP) && S.big_split &&
+                       S.k > big_split_j0(S.kp) + 2;
+  if (S.tq4 && S.kp == kTq4KP && !S.jacobi) {
+    // (Bs <= 2^19: the solve addresses a sub-batch's records with 32-bit byte offsets)
+    const long long cap = std::min<long long>(S.tq4_sub > 0 ? S.tq4_sub : nb, 1 << 19);
+    const long long Bs = std::min<long long>(sub_batch(nb, cap), 1 << 19);
+    // (+1: the spare record of solve_tq40_kernel's lanes past the sub-batch)
+    HIPCHK(S.wsa.ensure((size_t)(Bs + 1) * 8 * AsmRecord<kTq4KP>::WORDS));
+    double *rec = S.wsa.as<double>();
+    if (Bs >= nb) {  // the whole batch: timed between b2 and dn (recorded anyway)
+      auto asm_ = [&]() {
+        return launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0, nb, ncnt, nidx, infob,
+                                      rec);
+      };
+      auto tq40 = [&]() { return launch_solve_tq40(S.stream, S.kp, c, sd, g0, nb, rec, infob); };
+      HIPCHK(kt_pair(S.stream, b2, KT_ASSEMBLE_RECORD, nb, dn, KT_SOLVE_TQ40, nb, asm_, tq40));
+      return CWBL_OK;
+    }
+    for (long long s0 = 0; s0 < nb; s0 += Bs) {
+      const int ns = (int)std::min<long long>(Bs, nb - s0);
+      HIPCHK(kt_begin(S.stream, &kt));
+      HIPCHK(launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,
+                                    nidx + s0 * list_cap, infob + s0, rec));
+      HIPCHK(kt_end(S.stream, kt, KT_ASSEMBLE_RECORD, ns));
+      HIPCHK(kt_begin(S.stream, &kt));
+      HIPCHK(launch_solve_tq40(S.stream, S.kp, c, sd, g0 + s0, ns, rec, infob + s0));
+      HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ40, ns));
+    }
+    return CWBL_OK;
+  }
+  if (handoff) {
+    // BigHandoff<128, 64> is 134.7 KB per point (13 GB at the default 98 304-point
+    // sub-batch, outside workspace_bytes); the sub-batch is also bounded by the hand-off
+    // budget (cwbl_init: workspace_bytes when the caller gave one, else 13 GB or 40% of the
+    // free device memory)
+    const size_t rec_bytes = (size_t)8 * (S.kp == 96 ? BigHandoff<96, 32>::WORDS
+                                                     : BigHandoff<kBigSplitKP, kBigJ0>::WORDS);
+    const long long fit = std::max<long long>(
+        kListLanes, (long long)(S.handoff_budget / rec_bytes) / kListLanes * kListLanes);
+    const long long Bs = sub_batch(nb, std::min<long long>(S.big_sub, fit));
+    HIPCHK(S.wsa.ensure((size_t)Bs * rec_bytes));
+    for (long long s0 = 0; s0 < nb; s0 += Bs) {
+      const int ns = (int)std::min<long long>(Bs, nb - s0);
+      HIPCHK(kt_begin(S.stream, &kt));
+      HIPCHK(launch_big_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,
+                                nidx + s0 * list_cap, infob + s0, S.wsa.as<double>()));
+      HIPCHK(kt_end(S.stream, kt, KT_BIG_HANDOFF, ns));
+      HIPCHK(kt_begin(S.stream, &kt));
+      HIPCHK(launch_solve_tqb_tail(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
+                                   infob + s0));
+      HIPCHK(kt_end(S.stream, kt, KT_TQB_TAIL, ns));
+    }
+    return CWBL_OK;
+  }
+  HIPCHK(kt_begin(S.stream, &kt));
+  if (S.kp > kMaxWaveKP) {
+    HIPCHK(launch_solve_tq_big(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
+                               nullptr, nullptr, nullptr, nullptr, nullptr, infob));
+    HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ_BIG, nb));
+  } else if (S.jacobi) {
+    HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, ncnt, nidx, infob));
+    HIPCHK(kt_end(S.stream, kt, KT_SOLVE_JACOBI, nb));
+  } else {
+    HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, infob));
+    HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ, nb));
+  }
+  return CWBL_OK;
+}
+
+// After the last batch: the info of the open window, tune_q on the resident slab
+// (letkf_driver's Q species post-step, :253-278), the host slab's var back, one
+// synchronisation, and the statistics.
+int finish_call(VarCall &v, cwbl_stats &st) {
+  DevStats *dst = S.stats.as<DevStats>();
+  if (v.npts > v.win0)
+    HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), (int)(v.npts - v.win0), dst));
+  int ev = v.ev;
+  if (v.vp->tune_q) {
+    hipEvent_t a, b;
+    HIPCHK(event(ev, &a));
+    HIPCHK(event(ev + 1, &b));
+    HIPCHK(hipEventRecord(a, S.stream));
+    int kt;
+    HIPCHK(kt_begin(S.stream, &kt));
+    HIPCHK(launch_tune_q(S.stream, v.sd, S.k));
+    HIPCHK(kt_end(S.stream, kt, KT_TUNE_Q, v.npts));
+    HIPCHK(hipEventRecord(b, S.stream));
+    v.solve_ev.push_back({ev, ev + 1});
+    ev += 2;
+  }
+  hipEvent_t e_end, e_back;
+  HIPCHK(event(ev, &e_end));
+  HIPCHK(event(ev + 1, &e_back));
+  if (v.host && !v.piped_back && !v.bounce)
+    HIPCHK(hipMemcpyAsync(v.sl->var, S.svar.p, v.bvar, hipMemcpyDeviceToHost, S.stream));
+  if (v.piped_back) {  // the call returns after the last batch's copy back
+    HIPCHK(hipEventRecord(e_back, S.d2h));
+    HIPCHK(hipStreamWaitEvent(S.stream, e_back, 0));
+  }
+  const long long nbat = (long long)v.plan.size();
+  if (v.bounce && v.piped_back)  // drain the last batches
+    for (long long bj = std::max<long long>(0, nbat - (State::kSlots - 1)); bj < nbat; ++bj)
+      if (int rc = bounce_drain(v, bj)) return rc;
+  if (v.bounce && !v.piped_back)  // the whole slab back (after tune_q, or a staggered slab)
+    if (int rc = bounce_whole(v, false)) return rc;
+  HIPCHK(hipEventRecord(e_end, S.stream));
+  DevStats ds;
+  HIPCHK(hipMemcpyAsync(&ds, S.stats.p, sizeof ds, hipMemcpyDeviceToHost, S.stream));
+  HIPCHK(hipStreamSynchronize(S.stream));
+  kt_collect();
+
+  st.solved = (long long)ds.solved;
+  st.nobs_sum = (long long)ds.nobs_sum;
+  st.lz_truncated = (long long)ds.lz_truncated;
+  st.nonconverged = (long long)ds.nonconverged;
+  st.sweeps_sum = (long long)ds.sweeps_sum;
+  st.max_p = (int)ds.max_p;
+  st.max_sweeps = (int)ds.max_sweeps;
+  st.ms_prep = elapsed(0, 1);
+  for (auto &p : v.search_ev) st.ms_search += elapsed(p.first, p.second);
+  for (auto &p : v.solve_ev) st.ms_solve += elapsed(p.first, p.second);
+  // copies: x, y, alt (+ var when not piped) before the batches, var back after the last
+  // solve; piped transfers overlap the batches and are not counted here
+  st.ms_copy = elapsed(1, 2) + (v.host && !v.piped_back ? elapsed(ev - 1, ev) : 0.0f);
+  if (v.bounce) st.ms_copy = g_bounce_ms;  // the host threads' bounce copies
+  return CWBL_OK;
+}
+
 }  // namespace
 
 int set_last_error(int code, const char *msg) {
@@ -756,7 +1204,6 @@ int cwbl_init(const cwbl_init_params *p) {
   }
   HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.sstream, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&S.tstream, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.h2d, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&S.d2h, hipStreamNonBlocking));
   {
@@ -773,12 +1220,7 @@ int cwbl_init(const cwbl_init_params *p) {
   S.jacobi = false;
   S.tq4 = 1;
   S.tq4_sub = 0;
-  // r4: one stream by default.  With the r3 kernels the two-stream record path measures a
-  // tie (C2 58.7-59.2 M pts/s either way, HISTORY.md §3 item 6), and serial launches keep each
-  // kernel's duration its own (the per-kernel timing and the roofline read it).
-  S.tq40_streams = false;
   S.big_split = true;
-  S.band = false;
   // (C4 per variable, r3: 32 k points 2.42 s, 16 k 2.47, 64 k 2.41, 96 k 2.39, 128 k 2.39)
   S.big_sub = 98304;
   S.binned = true;
@@ -818,18 +1260,13 @@ int cwbl_set_option(int option, long long value) {
       if (!range(0, 1 << 19)) break;
       S.tq4_sub = value;
       return CWBL_OK;
-    case CWBL_OPT_SPLIT40_STREAMS:
-      if (!range(0, 1)) break;
-      S.tq40_streams = value != 0;
-      return CWBL_OK;
     case CWBL_OPT_SEARCH:
       if (!range(0, 1)) break;
       S.binned = value == 0;
       return CWBL_OK;
     case CWBL_OPT_BIG_PATH:
-      if (!range(0, 2)) break;
-      S.big_split = value >= 1;  // (2 at k <= 96: the hand-off path, as 1)
-      S.band = value == 2;
+      if (!range(0, 1)) break;
+      S.big_split = value == 1;
       return CWBL_OK;
     case CWBL_OPT_BIG_BATCH:
       if (!range(64, 1LL << 24)) break;
@@ -988,538 +1425,94 @@ int cwbl_analyze_var(const cwbl_var_params *vp, const cwbl_slab *sl, cwbl_stats 
   if (npts >= (1LL << 32))  // the kernels enumerate a slab's points in 32 bits
     return fail(CWBL_ERR_ARG, "slab of %lld points: at most 2^32 - 1 per call", npts);
   st.points = npts;
-
-  hipEvent_t e0, e1;
-  HIPCHK(event(0, &e0));
-  HIPCHK(hipEventRecord(e0, S.stream));
-  // ---- trees (cached per obs set) + column tables ------------------------------------------
-  std::vector<TreeDesc> descs;
-  int list_cap = 0;
-  int max_depth = 1;
-  if (int rc = build_family(0, vp, descs, list_cap, max_depth)) return rc;
-  if (int rc = build_family(1, vp, descs, list_cap, max_depth)) return rc;
-  const int nt = (int)descs.size();
-  st.ntrees = nt;
-  if (nt == 0 || npts == 0) {  // `if(all(.not. succeed)) cycle` (:66)
-    HIPCHK(hipStreamSynchronize(S.stream));
-    st.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  auto finish = [&]() {
+    st.ms_total =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     if (stats) *stats = st;
     return CWBL_OK;
-  }
-  for (const TreeDesc &d : descs) st.q1_undefined += d.q1_undef ? npts : 0;
-  HIPCHK(S.tdesc.ensure(descs.size() * sizeof(TreeDesc)));
-  HIPCHK(hipMemcpyAsync(S.tdesc.p, descs.data(), descs.size() * sizeof(TreeDesc),
-                        hipMemcpyHostToDevice, S.stream));
-  HIPCHK(event(1, &e1));
-  HIPCHK(hipEventRecord(e1, S.stream));
+  };
 
-  // ---- slab ---------------------------------------------------------------------------------
-  const long long L = (long long)sl->nx * sl->ny * sl->nz;
-  SlabDev sd{};
-  sd.nx = sl->nx; sd.ny = sl->ny; sd.nz = sl->nz; sd.alt_nx = sl->alt_nx;
-  sd.alt_ny = sl->alt_ny; sd.ix_lim = sl->ix_lim; sd.iy_lim = sl->iy_lim; sd.L = L;
-  const size_t bxy = (size_t)sl->nx * sl->ny * 4;
-  const size_t balt = (size_t)sl->alt_nx * sl->alt_ny * sl->nz * 4;
-  const size_t bvar = (size_t)L * S.k * 4;
-  hipEvent_t e2;
-  HIPCHK(event(2, &e2));
-  // Host-memory slab: x, y and alt go over first; var goes over batch by batch on its own
-  // stream (S.h2d) when a batch's points are contiguous in every member plane (the analysed
-  // region is the whole horizontal slab, ix_lim = nx and iy_lim = ny: point g is var word
-  // g + L m), and comes back batch by batch behind each batch's last solve (S.d2h), so the
-  // PCIe transfers overlap the kernels; otherwise (staggered U/V bounds) var moves whole.
-  const bool host = sl->memory != CWBL_MEM_DEVICE;
-  const bool piped = host && sl->ix_lim == sl->nx && sl->iy_lim == sl->ny;
-  const bool piped_back = piped && !vp->tune_q;  // tune_q touches the whole slab afterwards
-  // pageable var (a Fortran host's ordinary arrays): copies from pageable memory are staged
-  // by the runtime and do not overlap, so var goes through the library's page-locked bounce
-  // slots instead, filled / drained by host threads while the GPU runs other batches
-  bool bounce = host && bvar > 0 && !host_pinned(sl->var);
-  // A pageable var is page-locked in place for the call (hipHostRegister, undone on return)
-  // and then copied like page-locked memory: r4, C2 from pageable numpy arrays 58.7 M pts/s
-  // against 58.2 M from page-locked ones and 50.8 M through the bounce slots, whose host
-  // copies stall the pipeline.  The slots remain the fallback when the registration fails
-  // (and CWBL_OPT_PAGEABLE = 1 forces them).
-  bool registered = false;
-  if (bounce && S.pageable_register) {
-    if (hipHostRegister(sl->var, bvar, hipHostRegisterDefault) == hipSuccess) {
-      registered = true;
-      bounce = false;
-    } else {
-      (void)hipGetLastError();
-    }
-  }
-  struct Unregister {  // on every return path, once no queued copy can still touch var
-    bool on; void *p;
+  VarCall v;
+  v.vp = vp;
+  v.sl = sl;
+  v.npts = npts;
+  struct Unregister {  // a page-locked-in-place var, on every return path, once no queued
+    VarCall &v;        // copy can still touch it
     ~Unregister() {
-      if (!on) return;
+      if (!v.registered) return;
       (void)hipStreamSynchronize(S.h2d);
       (void)hipStreamSynchronize(S.d2h);
       (void)hipStreamSynchronize(S.stream);
       (void)hipGetLastError();
-      (void)hipHostUnregister(p);
+      (void)hipHostUnregister(v.sl->var);
     }
-  } unreg{registered, sl->var};
-  if (!host) {
-    sd.x = sl->x; sd.y = sl->y; sd.alt = sl->alt; sd.var = sl->var;
-  } else {
-    HIPCHK(stage(S.sx, sl->x, bxy, CWBL_MEM_HOST));
-    HIPCHK(stage(S.sy, sl->y, bxy, CWBL_MEM_HOST));
-    HIPCHK(stage(S.salt, sl->alt, balt, CWBL_MEM_HOST));
-    if (piped || bounce) HIPCHK(S.svar.ensure(bvar));
-    else HIPCHK(stage(S.svar, sl->var, bvar, CWBL_MEM_HOST));
-    sd.x = S.sx.as<float>(); sd.y = S.sy.as<float>(); sd.alt = S.salt.as<float>();
-    sd.var = S.svar.as<float>();
-  }
-  HIPCHK(hipEventRecord(e2, S.stream));
+  } unreg{v};
 
-  // ---- batches of {search, solve} ---------------------------------------------------------
-  const size_t per_pt = (size_t)list_cap * 4 + (size_t)nt * 4 + 8;
-  long long B = (long long)(S.ws_bytes / per_pt);
-  B = std::min<long long>(B, S.max_batch);
-  // at least ~6 batches while they stay above 64 k points: with few batches the first search
-  // and the last solve run alone (an 8-GPU rank's C2 share, 562 k points: 12.8 ms per step
-  // in batches of 141 k, 12.3 in batches of 94 k; the full grid is indifferent in 100-160 k)
-  if (!S.max_batch_set) B = std::min<long long>(B, std::max<long long>(npts / 6, 64000));
-  B = std::max<long long>(std::min<long long>(B, npts), 256);
-  B = std::min<long long>(B, 1 << 22);
-  // a batch's lists stay below 4 GiB: search_binned_kernel addresses them by 32-bit offsets
-  if (list_cap > 0)
-    B = std::min<long long>(B, (long long)((((size_t)1 << 32) - 1) / ((size_t)list_cap * 4)) /
-                                   kListLanes * kListLanes);
-  // Batch plan: the first batch's search cannot overlap a solve, so it is short (a lead of
-  // 1/lead_div of the points); the rest are equal (a short last batch is all tail) and
-  // whole list groups.
-  std::vector<std::pair<long long, int>> plan;  // (g0, nb)
-  {
-    const auto round_up = [](long long v) { return (v + kListLanes - 1) / kListLanes * kListLanes; };
-    long long lead = S.lead_div > 0 ? round_up(npts / S.lead_div) : 0;
-    if (lead < 4 * kListLanes || lead >= npts) lead = 0;
-    if (lead > 0) plan.push_back({0, (int)std::min<long long>(lead, B)});
-    const long long g1 = plan.empty() ? 0 : plan[0].second, rest = npts - g1;
-    const long long nrest = (rest + B - 1) / B;
-    long long Br = round_up((rest + nrest - 1) / nrest);
-    for (long long g = g1; g < npts; g += Br)
-      plan.push_back({g, (int)std::min<long long>(Br, npts - g)});
-    // (a short tail batch, the last batch's final 1/2 or 1/4 split off, measured within the
-    // run-to-run spread at the 8-rank share, r2: HISTORY.md §6)
-    B = 0;
-    for (const auto &b : plan) B = std::max<long long>(B, b.second);
+  hipEvent_t e0, e1, e2, e_ready;
+  HIPCHK(event(0, &e0));
+  HIPCHK(hipEventRecord(e0, S.stream));
+  if (int rc = plan_trees(v)) return rc;
+  st.ntrees = v.nt;
+  if (v.nt == 0 || npts == 0) {  // `if(all(.not. succeed)) cycle` (:66)
+    HIPCHK(hipStreamSynchronize(S.stream));
+    return finish();
   }
-  const long long nbat = (long long)plan.size();
-  // bounce slots: one batch (or one whole-slab chunk of B points) of k member rows each
-  const long long Bc = std::min<long long>(std::max<long long>(B, 1), std::max<long long>(L, 1));
-  int cev = 0;
-  std::vector<int> h2d_done, d2h_done;  // cevents of the bounce copies
-  // whole-slab moves through the slots (var not piped, or back after tune_q): chunk i of Bc
-  // points of every member row; up: fill slot i&1 (after its copy two chunks back), copy up on
-  // S.stream; down: copy chunk i down on S.stream, then drain chunk i-1 while it runs
-  auto bounce_whole = [&](bool up) -> int {
-    std::vector<int> evs;
-    long long pc0 = 0;
-    int pcn = 0;
-    const size_t pitch = (size_t)L * 4;
-    for (long long c0 = 0, i = 0; c0 < L; c0 += Bc, ++i) {
-      const int cn = (int)std::min<long long>(Bc, L - c0);
-      PinBuf &slot = up ? S.pin_in[i & 1] : S.pin_out[i & 1];
-      hipEvent_t e;
-      HIPCHK(cevent(cev, &e));
-      if (up) {
-        if (i >= 2) HIPCHK(hipEventSynchronize(S.cevents[evs[(size_t)i - 2]]));
-        bounce_rows(S.pool, slot.as<float>(), sl->var, L, c0, cn, S.k, true);
-        HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + c0, pitch, slot.p, (size_t)cn * 4,
-                                (size_t)cn * 4, (size_t)S.k, hipMemcpyHostToDevice, S.stream));
-      } else {
-        HIPCHK(hipMemcpy2DAsync(slot.p, (size_t)cn * 4, S.svar.as<float>() + c0, pitch,
-                                (size_t)cn * 4, (size_t)S.k, hipMemcpyDeviceToHost, S.stream));
-      }
-      HIPCHK(hipEventRecord(e, S.stream));
-      evs.push_back(cev++);
-      if (!up && i >= 1) {
-        HIPCHK(hipEventSynchronize(S.cevents[evs[(size_t)i - 1]]));
-        bounce_rows(S.pool, S.pin_out[(i - 1) & 1].as<float>(), sl->var, L, pc0, pcn, S.k, false);
-      }
-      pc0 = c0;
-      pcn = cn;
-    }
-    if (!up && !evs.empty()) {
-      HIPCHK(hipEventSynchronize(S.cevents[evs.back()]));
-      bounce_rows(S.pool, S.pin_out[(evs.size() - 1) & 1].as<float>(), sl->var, L, pc0, pcn,
-                  S.k, false);
-    }
-    return CWBL_OK;
-  };
-  if (registered) {  // the page-locked slots are only the fallback's: give them back
-    for (int i = 0; i < State::kSlots; ++i) {
-      S.pin_in[i].release();
-      S.pin_out[i].release();
-    }
-  }
-  if (bounce) {  // the slots the chosen path uses: whole-slab moves alternate two
-    const size_t slot_bytes = (size_t)Bc * S.k * 4;
-    const int nin = piped ? State::kSlots : 2, nout = piped_back ? State::kSlots : 2;
-    for (int i = 0; i < nin; ++i) HIPCHK(S.pin_in[i].ensure(slot_bytes));
-    for (int i = 0; i < nout; ++i) HIPCHK(S.pin_out[i].ensure(slot_bytes));
-    if (!piped)
-      if (int rc = bounce_whole(true)) return rc;
-  }
-  // piped bounce: batch b's columns into slot b % kSlots once the copy up of batch
-  // b - kSlots has left it; batch b's analysis out of its slot once its copy down is done
-  auto bounce_fill = [&](long long b) -> int {
-    if (b >= State::kSlots) HIPCHK(hipEventSynchronize(S.cevents[h2d_done[b - State::kSlots]]));
-    bounce_rows(S.pool, S.pin_in[b % State::kSlots].as<float>(), sl->var, L, plan[b].first,
-                plan[b].second, S.k, true);
-    return CWBL_OK;
-  };
-  auto bounce_drain = [&](long long b) -> int {
-    HIPCHK(hipEventSynchronize(S.cevents[d2h_done[b]]));
-    bounce_rows(S.pool, S.pin_out[b % State::kSlots].as<float>(), sl->var, L, plan[b].first,
-                plan[b].second, S.k, false);
-    return CWBL_OK;
-  };
-  const size_t bytes_cnt = (size_t)B * nt * 4;
-  const size_t bytes_idx =
-      (size_t)((B + kListLanes - 1) / kListLanes) * kListLanes * std::max(list_cap, 1) * 4;
-  HIPCHK(S.nbr_cnt.ensure(bytes_cnt));
-  HIPCHK(S.nbr_idx.ensure(bytes_idx));
-  if (nbat > 1) {
-    HIPCHK(S.nbr_cnt2.ensure(bytes_cnt));
-    HIPCHK(S.nbr_idx2.ensure(bytes_idx));
-  }
-  HIPCHK(S.flags.ensure((size_t)(B + 1) * sizeof(int)));
-  // bounding-box half-width of the binned search: the radius with a margin, so that every
-  // point with d2 <= r2 in fp32 lies inside
-  const float rbox = std::sqrt(search_r2()) * 1.0001f + 1e-5f;
-  HIPCHK(S.stats.ensure(sizeof(DevStats)));
-  HIPCHK(hipMemsetAsync(S.stats.p, 0, sizeof(DevStats), S.stream));
-  SolveConsts c = solve_consts((float)(S.k - 1) / vp->multi_infl,  // inflat (:68)
-                               vp->use_rtpp, vp->rtpp_alpha, vp->use_rtps, vp->rtps_alpha);
-  c.ntrees = nt;
-  c.list_cap = list_cap;
-  const TreeDesc *dtrees = S.tdesc.as<TreeDesc>();
-  DevStats *dst = S.stats.as<DevStats>();
-  // The searches run on S.sstream into two list buffers, the solves on S.stream: batch
-  // b + 1's search (latency-bound, integer/fp32) overlaps batch b's solve (FP64-bound).
-  // Search b waits for the inputs (e_ready) and for the solve of b - 2 (same buffer); solve b
-  // waits for search b.
-  hipEvent_t e_ready;  // inputs staged and the counters cleared
-  HIPCHK(event(3, &e_ready));
+  for (const TreeDesc &d : v.descs) st.q1_undefined += d.q1_undef ? npts : 0;
+  HIPCHK(event(1, &e1));
+  HIPCHK(hipEventRecord(e1, S.stream));
+  HIPCHK(event(2, &e2));
+  if (int rc = stage_slab(v)) return rc;
+  HIPCHK(hipEventRecord(e2, S.stream));
+  plan_batches(v);
+  if (int rc = stage_bounce(v)) return rc;
+  if (int rc = alloc_call_buffers(v)) return rc;
+  HIPCHK(event(3, &e_ready));  // inputs staged and the counters cleared
   HIPCHK(hipEventRecord(e_ready, S.stream));
   HIPCHK(hipStreamWaitEvent(S.sstream, e_ready, 0));
-  int ev = 4;
-  std::vector<std::pair<int, int>> search_ev, solve_ev;
-  std::vector<int> done_ev;
-  // Record path with the solves on their own stream (S.tstream): solve_tq40_kernel of a
-  // record batch overlaps the assembly of the next one (the assembly keeps the matrix pipe
-  // busy, the four-point solve is latency-bound).  Two record and two info buffers; an
-  // assembly waits for the solve two record batches back (record reuse) and for the info
-  // reduction two search batches back (info reuse).
-  const bool band_path = S.kp == kBigSplitKP && S.band && S.k > 96;
-  const bool big_split_path = !band_path && (S.kp == 96 || S.kp == kBigSplitKP) && S.big_split &&
-                              S.k > big_split_j0(S.kp) + 2;
-  // (r4, measured and dropped: the same two-stream scheme for the k > 64 split path, the
-  // tail of a hand-off sub-batch beside the next sub-batch's 256-thread kernel: +0.5%)
-  const bool conc = S.tq40_streams && S.tq4 && S.kp == kTq4KP && !S.jacobi;
-  int nrec = 0;                 // record batches so far
-  std::vector<int> rec_done;    // cevent after each record batch's solve (on S.tstream)
-  std::vector<int> info_done;   // cevent after each search batch's info reduction
-  // one-stream path: the info of a window of up to S.info_window points (the whole call
-  // below that), reduced once per window; the two-stream record path alternates two
-  // batch-sized buffers, reduced per batch
-  const long long info_cap =
-      conc ? B : std::max<long long>(B, std::min<long long>(npts, S.info_window));
-  HIPCHK(S.info.ensure((size_t)info_cap * sizeof(int2)));
-  if (conc) HIPCHK(S.info2.ensure((size_t)B * sizeof(int2)));
-  long long win0 = 0;  // first point of the current info window (one stream)
+
+  // The searches run on S.sstream into two list buffers, the solves on S.stream: batch b + 1's
+  // search (latency-bound, integer / fp32) overlaps batch b's solve (FP64-bound).  Search b
+  // waits for the inputs and for the solve of b - 2 (same buffer); solve b waits for search b.
+  const long long nbat = (long long)v.plan.size();
   for (long long bi = 0; bi < nbat; ++bi) {
-    const long long g0 = plan[bi].first;
-    const int nb = plan[bi].second;
-    if (!conc && g0 + nb - win0 > info_cap) {  // reduce the window; S.stream orders the reuse
-      HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), (int)(g0 - win0), dst));
-      win0 = g0;
+    const long long g0 = v.plan[bi].first;
+    const int nb = v.plan[bi].second;
+    if (g0 + nb - v.win0 > v.info_cap) {  // close the info window; S.stream orders the reuse
+      HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), (int)(g0 - v.win0),
+                                S.stats.as<DevStats>()));
+      v.win0 = g0;
     }
-    int2 *const infob = S.info.as<int2>() + (conc ? 0 : g0 - win0);  // this batch's info
+    int2 *const infob = S.info.as<int2>() + (g0 - v.win0);  // this batch's info
     int *ncnt = (bi & 1) ? S.nbr_cnt2.as<int>() : S.nbr_cnt.as<int>();
     int *nidx = (bi & 1) ? S.nbr_idx2.as<int>() : S.nbr_idx.as<int>();
-    hipEvent_t a, b, b2, cc, dn;
-    HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b)); HIPCHK(event(ev + 2, &b2));
-    HIPCHK(event(ev + 3, &cc)); HIPCHK(event(ev + 4, &dn));
-    // (timing experiment: CWBL_DEBUG_SERIAL=1 runs the searches on the solve stream, so
-    // neither kernel shares the GPU with the other)
-    hipStream_t ss = S.serial_search ? S.stream : S.sstream;
-    if (bi >= 2) HIPCHK(hipStreamWaitEvent(ss, S.events[done_ev[bi - 2]], 0));
-    HIPCHK(hipEventRecord(a, ss));
-    int kt;
-    if (S.binned) {  // bins; the tree search redoes the points whose lists pass max_lz
-      int *fcnt = S.flags.as<int>(), *fidx = fcnt + 1;
-      HIPCHK(hipMemsetAsync(fcnt, 0, sizeof(int), ss));
-      HIPCHK(kt_begin(ss, &kt));
-      HIPCHK(launch_search_binned(ss, dtrees, nt, list_cap, c.r2, rbox, sd, g0, nb, ncnt, nidx,
-                                  fcnt, fidx));
-      HIPCHK(kt_end(ss, kt, KT_SEARCH_BINNED, nb));
-      HIPCHK(kt_begin(ss, &kt));
-      HIPCHK(launch_search_flagged(ss, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb, fcnt,
-                                   fidx, ncnt, nidx, dst));
-      HIPCHK(kt_end(ss, kt, KT_SEARCH_FLAGGED, 0));
-    } else {
-      HIPCHK(kt_begin(ss, &kt));
-      HIPCHK(launch_search(ss, dtrees, nt, max_depth, list_cap, c.r2, sd, g0, nb, ncnt,
-                           nidx, nullptr, dst));
-      HIPCHK(kt_end(ss, kt, KT_SEARCH_TREE, nb));
-    }
-    HIPCHK(hipEventRecord(b, ss));
+    const int ev = v.ev;
+    hipEvent_t a, b, b2, dn;
+    HIPCHK(event(ev, &a));
+    HIPCHK(event(ev + 1, &b));
+    HIPCHK(event(ev + 2, &b2));
+    HIPCHK(event(ev + 3, &dn));
+    if (int rc = search_batch(v, bi, ncnt, nidx, a, b)) return rc;
     HIPCHK(hipStreamWaitEvent(S.stream, b, 0));
-    if (piped) {  // this batch's var columns: k rows of nb floats, member pitch L
-      hipEvent_t hv;
-      const int hv_i = cev++;
-      HIPCHK(cevent(hv_i, &hv));
-      const size_t pitch = (size_t)L * 4;
-      if (bounce) {  // slot bi % kSlots, filled before this batch (bounce_fill)
-        if (bi == 0)
-          if (int rc = bounce_fill(0)) return rc;
-        HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + g0, pitch,
-                                S.pin_in[bi % State::kSlots].p, (size_t)nb * 4, (size_t)nb * 4,
-                                (size_t)S.k, hipMemcpyHostToDevice, S.h2d));
-      } else {
-        HIPCHK(hipMemcpy2DAsync(S.svar.as<float>() + g0, pitch, sl->var + g0, pitch,
-                                (size_t)nb * 4, (size_t)S.k, hipMemcpyHostToDevice, S.h2d));
-      }
-      HIPCHK(hipEventRecord(hv, S.h2d));
-      h2d_done.push_back(hv_i);
-      HIPCHK(hipStreamWaitEvent(S.stream, hv, 0));
-    }
+    if (v.piped)
+      if (int rc = upload_batch_var(v, bi)) return rc;
     HIPCHK(hipEventRecord(b2, S.stream));
-    if (band_path) {
-      // band_head_kernel (assembly + 15 panel block reflectors to a band of half-bandwidth 8)
-      // -> workspace -> band_tail_kernel (chase, quadrature, back-transform), in sub-batches of
-      // Bs points (a multiple of kListLanes) bounded by the hand-off budget
-      const size_t rec_bytes = band_record_bytes();
-      const long long fit = std::max<long long>(
-          kListLanes, (long long)(S.handoff_budget / rec_bytes) / kListLanes * kListLanes);
-      const long long cap = std::min<long long>(S.big_sub, fit);
-      const long long nsub = (nb + cap - 1) / cap;
-      long long Bs = (nb + nsub - 1) / nsub;
-      Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
-      HIPCHK(S.wsa.ensure((size_t)Bs * rec_bytes));
-      for (long long s0 = 0; s0 < nb; s0 += Bs) {
-        const int ns = (int)std::min<long long>(Bs, nb - s0);
-        HIPCHK(kt_begin(S.stream, &kt));
-        HIPCHK(launch_band_head(S.stream, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,
-                                nidx + s0 * list_cap, infob + s0, S.wsa.as<double>()));
-        HIPCHK(kt_end(S.stream, kt, KT_BAND_HEAD, ns));
-        HIPCHK(kt_begin(S.stream, &kt));
-        HIPCHK(launch_band_tail(S.stream, c, sd, g0 + s0, ns, S.wsa.as<double>(), infob + s0));
-        HIPCHK(kt_end(S.stream, kt, KT_BAND_TAIL, ns));
-      }
-    } else if (big_split_path) {
-      // 256-thread assembly + first kBigJ0 steps -> workspace -> one-wavefront tail, in
-      // hand-off batches of Bs points (a multiple of kListLanes; BigHandoff<128, 64> is
-      // 134.7 KB per point, 13 GB at the default 98 304, outside workspace_bytes)
-      // the sub-batch is also bounded by the hand-off budget (cwbl_init: workspace_bytes
-      // when the caller gave one, else 13 GB or 40% of the free device memory)
-      const size_t rec_bytes = (size_t)8 * (S.kp == 96 ? BigHandoff<96, 32>::WORDS
-                                                       : BigHandoff<kBigSplitKP, kBigJ0>::WORDS);
-      const long long fit = std::max<long long>(
-          kListLanes, (long long)(S.handoff_budget / rec_bytes) / kListLanes * kListLanes);
-      const long long cap = std::min<long long>(S.big_sub, fit);
-      const long long nsub = (nb + cap - 1) / cap;
-      long long Bs = (nb + nsub - 1) / nsub;
-      Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
-      HIPCHK(S.wsa.ensure((size_t)Bs * rec_bytes));
-      for (long long s0 = 0; s0 < nb; s0 += Bs) {
-        const int ns = (int)std::min<long long>(Bs, nb - s0);
-        HIPCHK(kt_begin(S.stream, &kt));
-        HIPCHK(launch_big_handoff(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns, ncnt + s0 * nt,
-                                  nidx + s0 * list_cap, infob + s0,
-                                  S.wsa.as<double>()));
-        HIPCHK(kt_end(S.stream, kt, KT_BIG_HANDOFF, ns));
-        HIPCHK(kt_begin(S.stream, &kt));
-        HIPCHK(launch_solve_tqb_tail(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
-                                     infob + s0));
-        HIPCHK(kt_end(S.stream, kt, KT_TQB_TAIL, ns));
-      }
-    } else if (S.kp > kMaxWaveKP) {
-      HIPCHK(kt_begin(S.stream, &kt));
-      HIPCHK(launch_solve_tq_big(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
-                                 nullptr, nullptr, nullptr, nullptr, nullptr,
-                                 infob));
-      HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ_BIG, nb));
-    } else if (S.jacobi) {
-      HIPCHK(kt_begin(S.stream, &kt));
-      HIPCHK(launch_solve_neighbors(S.stream, S.kp, dtrees, c, sd, g0, nb, ncnt, nidx,
-                                    infob));
-      HIPCHK(kt_end(S.stream, kt, KT_SOLVE_JACOBI, nb));
-    } else if (S.tq4 && S.kp == kTq4KP) {
-      // assembly -> workspace -> four-points-per-wave solve, in hand-off batches of Bs
-      // points (a multiple of kListLanes, so a batch's neighbour lists start on a group)
-      // (Bs <= 2^19: the solve addresses a batch's records with 32-bit byte offsets), the
-      // search batch split evenly
-      const long long cap = std::min<long long>(S.tq4_sub > 0 ? S.tq4_sub : nb, 1 << 19);
-      const long long nsub = (nb + cap - 1) / cap;
-      long long Bs = (nb + nsub - 1) / nsub;
-      Bs = std::max<long long>(kListLanes, (Bs + kListLanes - 1) / kListLanes * kListLanes);
-      Bs = std::min<long long>(Bs, 1 << 19);
-      // (+1: the spare record of solve_tq40_kernel's lanes past the batch)
-      const size_t wbytes = (size_t)(Bs + 1) * 8 * AsmRecord<kTq4KP>::WORDS;
-      HIPCHK(S.wsa.ensure(wbytes));
-      if (conc) HIPCHK(S.wsa2.ensure(wbytes));
-      int2 *binfo = conc && (bi & 1) ? S.info2.as<int2>() : infob;
-      if (conc && bi >= 2)  // this search batch's info buffer: reduced two batches back
-        HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[info_done[bi - 2]], 0));
-      for (long long s0 = 0; s0 < nb; s0 += Bs) {
-        const int ns = (int)std::min<long long>(Bs, nb - s0);
-        if (conc) {
-          double *recp = (nrec & 1) ? S.wsa2.as<double>() : S.wsa.as<double>();
-          if (nrec >= 2)  // this record buffer: solved two record batches back
-            HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[rec_done[nrec - 2]], 0));
-          HIPCHK(kt_begin(S.stream, &kt));
-          HIPCHK(launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
-                                        ncnt + s0 * nt, nidx + s0 * list_cap, binfo + s0,
-                                        recp));
-          HIPCHK(kt_end(S.stream, kt, KT_ASSEMBLE_RECORD, ns));
-          hipEvent_t ea, et;
-          HIPCHK(cevent(cev, &ea));
-          HIPCHK(cevent(cev + 1, &et));
-          HIPCHK(hipEventRecord(ea, S.stream));
-          HIPCHK(hipStreamWaitEvent(S.tstream, ea, 0));
-          HIPCHK(kt_begin(S.tstream, &kt));
-          HIPCHK(launch_solve_tq40(S.tstream, S.kp, c, sd, g0 + s0, ns, recp, binfo + s0));
-          HIPCHK(kt_end(S.tstream, kt, KT_SOLVE_TQ40, ns));
-          HIPCHK(hipEventRecord(et, S.tstream));
-          rec_done.push_back(cev + 1);
-          cev += 2;
-          ++nrec;
-        } else if (ns == nb) {  // the whole batch: timed between b2 and dn (recorded anyway)
-          auto asm_ = [&]() {
-            return launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0, ns, ncnt, nidx,
-                                          infob, S.wsa.as<double>());
-          };
-          auto tq40 = [&]() {
-            return launch_solve_tq40(S.stream, S.kp, c, sd, g0, ns, S.wsa.as<double>(),
-                                     infob);
-          };
-          HIPCHK(kt_pair(S.stream, b2, KT_ASSEMBLE_RECORD, ns, dn, KT_SOLVE_TQ40, ns, asm_, tq40));
-        } else {
-          HIPCHK(kt_begin(S.stream, &kt));
-          HIPCHK(launch_assemble_record(S.stream, S.kp, dtrees, c, sd, g0 + s0, ns,
-                                        ncnt + s0 * nt, nidx + s0 * list_cap,
-                                        infob + s0, S.wsa.as<double>()));
-          HIPCHK(kt_end(S.stream, kt, KT_ASSEMBLE_RECORD, ns));
-          HIPCHK(kt_begin(S.stream, &kt));
-          HIPCHK(launch_solve_tq40(S.stream, S.kp, c, sd, g0 + s0, ns, S.wsa.as<double>(),
-                                   infob + s0));
-          HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ40, ns));
-        }
-      }
-    } else {
-      HIPCHK(kt_begin(S.stream, &kt));
-      HIPCHK(launch_solve_tq(S.stream, S.kp, false, dtrees, c, sd, g0, nb, ncnt, nidx,
-                             nullptr, nullptr, nullptr, nullptr, nullptr,
-                             infob));
-      HIPCHK(kt_end(S.stream, kt, KT_SOLVE_TQ, nb));
-    }
+    if (int rc = solve_batch_path(v, g0, nb, ncnt, nidx, infob, b2, dn)) return rc;
     HIPCHK(hipEventRecord(dn, S.stream));  // this batch's lists are free again
-    if (conc) {  // the solves and the info reduction of this batch on S.tstream
-      int2 *binfo = (bi & 1) ? S.info2.as<int2>() : S.info.as<int2>();
-      HIPCHK(launch_reduce_info(S.tstream, binfo, nb, dst));
-      HIPCHK(hipEventRecord(cc, S.tstream));
-      hipEvent_t ir;
-      HIPCHK(cevent(cev, &ir));
-      HIPCHK(hipEventRecord(ir, S.tstream));
-      info_done.push_back(cev++);
-    } else {  // the solve's end is dn's point on S.stream: no second event there
-      cc = dn;
-    }
-    if (piped_back) {  // the batch's analysis back to the caller behind its last solve
-      HIPCHK(hipStreamWaitEvent(S.d2h, cc, 0));
-      const size_t pitch = (size_t)L * 4;
-      if (bounce) {  // into slot bi % kSlots (drained kSlots - 1 batches later)
-        hipEvent_t dv;
-        const int dv_i = cev++;
-        HIPCHK(cevent(dv_i, &dv));
-        HIPCHK(hipMemcpy2DAsync(S.pin_out[bi % State::kSlots].p, (size_t)nb * 4,
-                                S.svar.as<float>() + g0, pitch, (size_t)nb * 4, (size_t)S.k,
-                                hipMemcpyDeviceToHost, S.d2h));
-        HIPCHK(hipEventRecord(dv, S.d2h));
-        d2h_done.push_back(dv_i);
-      } else {
-        HIPCHK(hipMemcpy2DAsync(sl->var + g0, pitch, S.svar.as<float>() + g0, pitch,
-                                (size_t)nb * 4, (size_t)S.k, hipMemcpyDeviceToHost, S.d2h));
-      }
-    }
-    if (bounce && piped) {  // host side while the GPU works: next batch in, batch bi - 2 out
+    if (v.piped_back)
+      if (int rc = return_batch_var(v, bi, dn)) return rc;
+    if (v.bounce && v.piped) {  // host side while the GPU works: next batch in, bi - 2 out
       if (bi + 1 < nbat)
-        if (int rc = bounce_fill(bi + 1)) return rc;
-      if (piped_back && bi >= State::kSlots - 1)
-        if (int rc = bounce_drain(bi - (State::kSlots - 1))) return rc;
+        if (int rc = bounce_fill(v, bi + 1)) return rc;
+      if (v.piped_back && bi >= State::kSlots - 1)
+        if (int rc = bounce_drain(v, bi - (State::kSlots - 1))) return rc;
     }
-    search_ev.push_back({ev, ev + 1});
-    solve_ev.push_back({ev + 2, conc ? ev + 3 : ev + 4});
-    done_ev.push_back(ev + 4);
-    ev += 5;
+    v.search_ev.push_back({ev, ev + 1});
+    v.solve_ev.push_back({ev + 2, ev + 3});
+    v.done_ev.push_back(ev + 3);
+    v.ev += 4;
   }
-  if (conc && !info_done.empty())  // everything below follows the last solve and reduction
-    HIPCHK(hipStreamWaitEvent(S.stream, S.cevents[info_done.back()], 0));
-  if (!conc && npts > win0)
-    HIPCHK(launch_reduce_info(S.stream, S.info.as<int2>(), (int)(npts - win0), dst));
-  if (vp->tune_q) {  // letkf_driver's Q species post-step (:253-278), on the resident slab
-    hipEvent_t a, b;
-    HIPCHK(event(ev, &a)); HIPCHK(event(ev + 1, &b));
-    HIPCHK(hipEventRecord(a, S.stream));
-    int kt;
-    HIPCHK(kt_begin(S.stream, &kt));
-    HIPCHK(launch_tune_q(S.stream, sd, S.k));
-    HIPCHK(kt_end(S.stream, kt, KT_TUNE_Q, npts));
-    HIPCHK(hipEventRecord(b, S.stream));
-    solve_ev.push_back({ev, ev + 1});
-    ev += 2;
-  }
-  hipEvent_t e_end, e_back;
-  HIPCHK(event(ev, &e_end));
-  HIPCHK(event(ev + 1, &e_back));
-  if (host && !piped_back && !bounce)
-    HIPCHK(hipMemcpyAsync(sl->var, S.svar.p, bvar, hipMemcpyDeviceToHost, S.stream));
-  if (piped_back) {  // the call returns after the last batch's copy back
-    HIPCHK(hipEventRecord(e_back, S.d2h));
-    HIPCHK(hipStreamWaitEvent(S.stream, e_back, 0));
-  }
-  if (bounce && piped_back)  // drain the last batches
-    for (long long bj = std::max<long long>(0, nbat - (State::kSlots - 1)); bj < nbat; ++bj)
-      if (int rc = bounce_drain(bj)) return rc;
-  if (bounce && !piped_back)  // the whole slab back (after tune_q, or a staggered slab)
-    if (int rc = bounce_whole(false)) return rc;
-  HIPCHK(hipEventRecord(e_end, S.stream));
-  DevStats ds;
-  HIPCHK(hipMemcpyAsync(&ds, S.stats.p, sizeof ds, hipMemcpyDeviceToHost, S.stream));
-  HIPCHK(hipStreamSynchronize(S.stream));
-  kt_collect();
-
-  st.solved = (long long)ds.solved;
-  st.nobs_sum = (long long)ds.nobs_sum;
-  st.lz_truncated = (long long)ds.lz_truncated;
-  st.nonconverged = (long long)ds.nonconverged;
-  st.sweeps_sum = (long long)ds.sweeps_sum;
-  st.max_p = (int)ds.max_p;
-  st.max_sweeps = (int)ds.max_sweeps;
-  st.ms_prep = elapsed(0, 1);
-  for (auto &p : search_ev) st.ms_search += elapsed(p.first, p.second);
-  if (conc && !solve_ev.empty()) {
-    // the batches' solves overlap (assembly b + 1 with solve b): their span, not their sum
-    // (tune_q's pair, if any, is the last entry and follows the span)
-    const size_t nsv = (size_t)nbat;
-    st.ms_solve = elapsed(solve_ev[0].first, solve_ev[nsv - 1].second);
-    for (size_t i = nsv; i < solve_ev.size(); ++i)
-      st.ms_solve += elapsed(solve_ev[i].first, solve_ev[i].second);
-  } else {
-    for (auto &p : solve_ev) st.ms_solve += elapsed(p.first, p.second);
-  }
-  // copies: x, y, alt (+ var when not piped) before the batches, var back after the last
-  // solve; piped transfers overlap the batches and are not counted here
-  st.ms_copy = elapsed(1, 2) + (host && !piped_back ? elapsed(ev - 1, ev) : 0.0f);
-  if (bounce) st.ms_copy = g_bounce_ms;  // the host threads' bounce copies
-  st.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
-  if (stats) *stats = st;
-  return CWBL_OK;
+  if (int rc = finish_call(v, st)) return rc;
+  return finish();
 }
 
 int cwbl_solve_batch(int npts, const long long *col_off, const float *yo, const float *yb,

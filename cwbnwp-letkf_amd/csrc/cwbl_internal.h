@@ -253,17 +253,6 @@ hipError_t launch_rows_handoff(hipStream_t s, const TreeDesc *trees, SolveConsts
 hipError_t launch_solve_tqb_tail(hipStream_t s, int kp, SolveConsts c, SlabDev slab,
                                  long long g0, int npts, double *ws, int2 *info);
 
-// The two-stage KP = 128 slab path (cwbl_band.hip; k = 97..128): band_head_kernel (256 threads
-// per point) assembles A and reduces it to a band of half-bandwidth 8 with 15 panel block
-// reflectors on the matrix cores; band_tail_kernel (one point per wavefront) chases the band to
-// tridiagonal form and finishes the solve.  One record of band_record_bytes() per point.
-hipError_t launch_band_head(hipStream_t s, const TreeDesc *trees, SolveConsts c, SlabDev slab,
-                            long long g0, int npts, const int *nbr_cnt, const int *nbr_idx,
-                            int2 *info, double *ws);
-hipError_t launch_band_tail(hipStream_t s, SolveConsts c, SlabDev slab, long long g0, int npts,
-                            double *ws, int2 *info);
-size_t band_record_bytes();
-
 // KP = 96, 128: one 256-thread workgroup per point (cwbl_tq_big.hip)
 hipError_t launch_solve_tq_big(hipStream_t s, int kp, bool assembled, const TreeDesc *trees,
                                SolveConsts c, SlabDev slab, long long g0, int npts,

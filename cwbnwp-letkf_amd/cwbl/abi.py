@@ -26,11 +26,11 @@ Q1_REPLICATE, Q1_PER_TYPE = 0, 1
 GTS_NVAR = {GTS_SOUND: 4, GTS_SYNOP: 5, GTS_GPSPW: 1, GTS_METAR: 5, GTS_SHIPS: 5}
 
 #: cwbl_set_option options (include/cwb_letkf_core.h)
-OPT_SOLVER, OPT_SPLIT40, OPT_SPLIT40_BATCH, OPT_SPLIT40_STREAMS, OPT_SEARCH = 1, 2, 3, 4, 5
+OPT_SOLVER, OPT_SPLIT40, OPT_SPLIT40_BATCH, OPT_SEARCH = 1, 2, 3, 5
 OPT_BIG_PATH, OPT_BIG_BATCH, OPT_PAGEABLE, OPT_BIN_DIV, OPT_LEAD_DIV, OPT_MAX_BATCH = 6, 7, 8, 9, 10, 11
 OPT_INFO_WINDOW = 12
 OPTIONS = {"solver": OPT_SOLVER, "split40": OPT_SPLIT40, "split40_batch": OPT_SPLIT40_BATCH,
-           "split40_streams": OPT_SPLIT40_STREAMS, "search": OPT_SEARCH,
+           "search": OPT_SEARCH,
            "big_path": OPT_BIG_PATH, "big_batch": OPT_BIG_BATCH, "pageable": OPT_PAGEABLE,
            "bin_div": OPT_BIN_DIV, "lead_div": OPT_LEAD_DIV, "max_batch": OPT_MAX_BATCH,
            "info_window": OPT_INFO_WINDOW}

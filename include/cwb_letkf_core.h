@@ -296,13 +296,11 @@ enum {
   CWBL_OPT_SPLIT40 = 2,        /* k = 17..40: 1 assembly record + four-point solve (default);
                                 * 0 the one-wavefront kernel */
   CWBL_OPT_SPLIT40_BATCH = 3,  /* points per record sub-batch of that path (0 = search batch) */
-  CWBL_OPT_SPLIT40_STREAMS = 4,/* 1: its four-point solve on a second stream (default 0) */
+                               /* (4: the r4 two-stream record path, removed in r6: a tie) */
   CWBL_OPT_SEARCH = 5,         /* 0 uniform bins + tree for truncated lists (default); 1 the
                                 * k-d tree walk for every point */
   CWBL_OPT_BIG_PATH = 6,       /* k = 65..128: 1 256-thread hand-off + one-wave tail (default);
-                                * 0 one 256-thread kernel; 2 two-stage at k = 97..128 (band
-                                * reduction on the matrix cores + one-wave bulge chase), the
-                                * hand-off path at k = 65..96 as with 1 */
+                                * 0 one 256-thread kernel */
   CWBL_OPT_BIG_BATCH = 7,      /* points per k > 64 sub-batch (>= 64; default 98 304) */
   CWBL_OPT_PAGEABLE = 8,       /* pageable host slab: 0 page-lock in place (default); 1 bounce
                                 * through the library's page-locked slots */

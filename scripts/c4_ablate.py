@@ -3,8 +3,6 @@ CWBL_DEBUG_TQ_STOP[:CWBL_DEBUG_TQ_STEPS] setting.  Needs the DEBUG_KNOBS library
 cwbnwp-letkf_amd debuglib`, loaded with CWBL_LIBRARY=cwbnwp-letkf_amd/lib_dbg/libcwbl.so); the
 release library ignores the variables.
 
-  --path 2 (two-stage band path; head: 1 assembly only, 5 without the panel QRs, 6 the QRs
-            without the trailing updates; tail: 2 the chase only, 3 chase + quadrature)
   --path 1 (hand-off path; hand-off kernel: 12 column staging only, 1 assembly only, 0:S the
             first S of its 64 steps; tail kernel: 2 its steps only, 3 steps + quadrature)
 
@@ -20,11 +18,10 @@ import torch  # noqa: E402
 from cwbl import abi, dist as cdist, synth  # noqa: E402
 
 args = sys.argv[1:]
-path = 2
+path = 1
 if args[:1] == ["--path"]:
     path, args = int(args[1]), args[2:]
-specs = args or (["0", "1", "5", "6", "2", "3"] if path == 2 else ["0", "12", "1", "0:16", "0:32",
-                                                                   "0:48", "2", "3"])
+specs = args or ["0", "12", "1", "0:16", "0:32", "0:48", "2", "3"]
 w = synth.make("c4", local_noise=True)
 dev = torch.device("cuda:0")
 types = [dict(family=1, type_id=w.radar_type, xyz=w.obs_xyz, obs=w.obs, hdxb=w.hdxb)]

@@ -663,50 +663,6 @@ def test_split_big_path_vs_one_kernel_and_oracle(k, sparse):
     assert rel <= INCR_TOL, rel
 
 
-@pytest.mark.parametrize("k,sparse", [(97, False), (101, True), (127, False), (128, False),
-                                      (128, True)])
-def test_band_path_vs_one_kernel_and_oracle(k, sparse):
-    """The two-stage KP = 128 path (big_path = 2: band_head_kernel reduces A to a band of
-    half-bandwidth 8 with 15 panel block reflectors on the matrix cores, band_tail_kernel
-    chases it to tridiagonal form and finishes the solve) against the one-kernel path on the
-    whole 30x30x50 grid (solved and obs counts equal, increments within 1e-6) and the oracle
-    on a 6x6-column block; k < 128 exercises the identity padding, the sparse obs set p < k
-    (exactly-zero reflectors); sub-batches of 1024 points."""
-    import ctypes as C
-    from cwbl import synth
-    w = synth.make("c4", scale=0.1, k=k)
-    if sparse:
-        keep = np.arange(w.obs.shape[0]) % 25 == 0
-        w.obs_xyz = np.ascontiguousarray(w.obs_xyz[keep])
-        w.obs = np.ascontiguousarray(w.obs[keep])
-        w.hdxb = np.ascontiguousarray(w.hdxb[:, keep])
-    out = {}
-    for mode in (0, 2):
-        _cores.clear()
-        c = abi.Core(w.k, device=0, options={"big_batch": 1024, "big_path": mode})
-        c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
-        var = w.var.copy()
-        st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
-        kt = c.kernel_times() if mode == 2 else None
-        c.finalize()
-        assert np.isfinite(var).all(), mode
-        assert st.nonconverged == 0 and st.solved > 0
-        out[mode] = (var, st.solved, st.nobs_sum)
-    assert out[0][1:] == out[2][1:]
-    rel = increment_rel_rms(out[2][0], out[0][0], w.var)
-    assert rel <= INCR_TOL, rel
-    j0, i0, nb = 12, 12, 6
-    sub = lambda a: np.ascontiguousarray(a[..., j0:j0 + nb, i0:i0 + nb])  # noqa: E731
-    ref = sub(w.var).copy()
-    ob = abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build()
-    rc = oracle().orc_analyze_var(w.k, 0, -5.0, 0, C.byref(ob), C.byref(w.vp),
-                                  C.byref(abi.make_slab(sub(w.x), sub(w.y), sub(w.alt), ref)),
-                                  16, C.byref(abi.Stats()))
-    assert rc == 0
-    rel = increment_rel_rms(sub(out[2][0]), ref, sub(w.var))
-    assert rel <= INCR_TOL, rel
-
-
 def test_info_window_rollover_matches_single_window():
     """The per-point solve info (solved flag, p) is reduced once per window of
     CWBL_OPT_INFO_WINDOW points (2^25 by default, so one window below 33.5 M points).  Small
