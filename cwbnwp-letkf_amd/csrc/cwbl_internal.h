@@ -116,10 +116,14 @@ constexpr int kQuadLevels31 = 12;
 constexpr int kQuadStride = 64;
 void quad_table(int level, double2 *out64, int nodes = kQuadNodes);
 // Rounds of 8 nodes (the last round's slot 7 is the exact T^-1 solve) solve_tq40_kernel runs
-// at a level: the (8 R - 1)-node rule is as accurate as the 31-node one up to level 12
-// (relative error <= 1e-15 at levels 1..3; tests/test_quadrature.py), 63 nodes above.
+// at a level: the fewest whose (8 R - 1)-node rule stays within 1e-12 relative error where the
+// 31-node rule does (levels 1..7), and the 31-node rule itself up to level 12, 63 nodes above
+// (tests/test_quadrature.py: 15 nodes <= 2.1e-13 to level 3, 23 nodes <= 6.4e-14 to level 5).
+// r6: 15 nodes at level 3 (C2: two thirds of the points, so nearly every wave of four) instead
+// of 23 — one quadrature round fewer per wave; the error stays ~1e7 below the fp32 rounding of
+// the analysis.
 __host__ __device__ constexpr int quad_rounds(int level) {
-  return level <= 2 ? 2 : level == 3 ? 3 : level <= kQuadLevels31 ? 4 : 8;
+  return level <= 3 ? 2 : level <= 5 ? 3 : level <= kQuadLevels31 ? 4 : 8;
 }
 // passes of the one-wavefront kernels' rule (31 nodes per pass + the exact solve)
 __host__ __device__ constexpr int quad_passes(int level) { return level <= kQuadLevels31 ? 1 : 2; }

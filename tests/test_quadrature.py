@@ -49,17 +49,33 @@ def test_rule_accuracy(lib, level):
 
 
 # solve_tq40_kernel runs 8 R - 1 nodes (R = quad_rounds(level), cwbl_internal.h: 2 rounds up to
-# level 2, 3 at level 3, 4 to level 12, 8 above) with the exact T^-1 solve in the last slot; a
+# level 3, 3 to level 5, 4 to level 12, 8 above) with the exact T^-1 solve in the last slot; a
 # wave runs the largest R its four points need, each point with its own level's table, so a
-# level-1 or level-2 point can run 23 or 63 nodes too.  The short rules must be as accurate
-# there as the 31-node one.
-@pytest.mark.parametrize("level,n", [(1, 15), (2, 15), (3, 23), (1, 23), (2, 23),
-                                     (1, 63), (2, 63), (3, 63)])
+# point can run a longer rule than its level needs.  Every short rule a level can run stays
+# within 1e-12 relative error (as the 31-node rule does to level 7).
+SHORT = {(1, 15): 1e-15, (2, 15): 1e-15, (3, 15): 5e-13, (1, 23): 2e-15, (2, 23): 2e-15,
+         (3, 23): 2e-15, (4, 23): 2e-15, (5, 23): 2e-13, (1, 63): 2e-15, (2, 63): 2e-15,
+         (3, 63): 2e-15, (5, 63): 2e-15}
+
+
+@pytest.mark.parametrize("level,n", sorted(SHORT))
 def test_short_rules_accuracy(lib, level, n):
     t2, w = table(lib, level, n)
     assert np.all(t2 > 0) and np.all(w > 0) and np.all(np.diff(t2) > 0)
     err = rule_error(t2, w, level)
-    assert err <= 2e-15, err
+    assert err <= SHORT[(level, n)], err
+
+
+def test_quad_rounds_stay_within_1e12():
+    """The rounds solve_tq40_kernel runs at each level (quad_rounds): every rule a wave can hand
+    a point of levels 1..7 (its own R or a larger one) is within 1e-12 (above, the 31-node
+    rule's own BOUND governs)."""
+    rounds = lambda L: 2 if L <= 3 else 3 if L <= 5 else 4 if L <= 12 else 8  # noqa: E731
+    lib_ = abi.load_library()
+    for L in range(1, 8):
+        for R in sorted({2, 3, 4, 8} & set(range(rounds(L), 9))):
+            err = rule_error(*table(lib_, L, 8 * R - 1), L)
+            assert err <= 1e-12, (L, R, err)
 
 
 # above level kQuadLevels31 (12) the one-wavefront kernels run a second pass (63 nodes) and
