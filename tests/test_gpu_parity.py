@@ -688,6 +688,31 @@ def test_info_window_rollover_matches_single_window():
         np.testing.assert_array_equal(var.view(np.uint32), runs[0][0].view(np.uint32))
 
 
+def test_bin_div_option_applies_to_cached_trees():
+    """CWBL_OPT_BIN_DIV set between two analyses of one obs set: the cached tree's bins are
+    rebuilt for the new divisor (the cache is keyed by it), so the second call searches bins
+    of r/1 and finds the same neighbour sets: equal solved / accepted-obs counts, increments
+    equal up to the fp64 summation order of the new column order."""
+    from cwbl import synth
+    w = synth.make("c2", seed=29, scale=0.1, nz=10)
+    _cores.clear()
+    c = abi.Core(w.k, device=0)
+    c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
+    outs = []
+    for div in (0, 1, 4, 0):
+        c.set_option("bin_div", div)
+        var = w.var.copy()
+        st = c.analyze_var(w.vp, abi.make_slab(w.x, w.y, w.alt, var))
+        outs.append((var, st.solved, st.nobs_sum, st.lz_truncated))
+    c.finalize()
+    _cores.clear()
+    assert outs[0][1] > 0
+    for var, *cnt in outs[1:]:
+        assert cnt == list(outs[0][1:])
+        assert increment_rel_rms(var, outs[0][0], w.var) <= 1e-10
+    np.testing.assert_array_equal(outs[3][0].view(np.uint32), outs[0][0].view(np.uint32))
+
+
 def test_tune_q_matches_reference():
     """letkf_tune_q on the device (cwbl_var_params.tune_q) against the reference's compiled
     letkf_tune_q (G5): bit for bit, including the Q3 NaN columns.  The single obs lies far
