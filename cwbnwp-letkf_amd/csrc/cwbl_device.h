@@ -620,6 +620,11 @@ __device__ __forceinline__ int stage_columns_pair(
     auto var_of = [&](int q) { return q - divn(q) * nvar; };
     auto gather_bg = [&](int col, f32x4 (&g)[VH / 2]) {
       const unsigned b0 = (unsigned)(col * KP + 2 * VH * half);
+      if (CWBL_DBG_STOP(c) == 13) {  // timing ablation: the assembly without the gathers
+#pragma unroll
+        for (int i = 0; i < VH / 2; ++i) g[i] = f32x4{1.0f, 1.0f, 1.0f, 1.0f};
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < VH / 2; ++i) g[i] = gld4(T.col_bg, b0 + 4u * (unsigned)quad(i));
     };
@@ -642,10 +647,12 @@ __device__ __forceinline__ int stage_columns_pair(
       const int col_a = (half ? slot_x : slot) * nvar + var_of(qa);
       f32x4 g[VH / 2];
       gather_bg(col_a, g);
-      const uint8_t okb = gld(T.col_ok, (unsigned)col_o);
-      const float err = gld(T.col_err, (unsigned)col_o);
-      const float omm = gld(T.col_omm, (unsigned)col_o);
-      const f32x4 rd = gld4(reinterpret_cast<const float *>(T.rdata), 4u * (unsigned)slot);
+      const bool nog = CWBL_DBG_STOP(c) == 13;  // (timing ablation, see gather_bg)
+      const uint8_t okb = nog ? 1 : gld(T.col_ok, (unsigned)col_o);
+      const float err = nog ? 1.0f : gld(T.col_err, (unsigned)col_o);
+      const float omm = nog ? 0.0f : gld(T.col_omm, (unsigned)col_o);
+      const f32x4 rd = nog ? f32x4{0.0f, 0.0f, 0.0f, 0.0f}
+                           : gld4(reinterpret_cast<const float *>(T.rdata), 4u * (unsigned)slot);
       const bool ok = qo < npairs && okb != 0;
       const float wv =
           error_inv(c.weight_function, err, slot_r2(rd, T.tree_dim, q0, q1, q2), ch.expt);

@@ -6,7 +6,11 @@ release library ignores the variables.
   --path 1 (hand-off path; hand-off kernel: 12 column staging only, 1 assembly only, 0:S the
             first S of its 64 steps; tail kernel: 2 its steps only, 3 steps + quadrature)
 
-Usage: python scripts/c4_ablate.py [--path N] [stop[:steps] ...]"""
+  --config c2 (the record path: assembly kernel 11 = staging only (no MFMA groups), 13 =
+            without the gathers, 1 = no record write; solve_tq40_kernel 5 = record loads
+            only, 4 = + phase 1, 2 = + phase 2, 3 = + quadrature)
+
+Usage: python scripts/c4_ablate.py [--config c2|c4] [--path N] [stop[:steps] ...]"""
 import json
 import os
 import sys
@@ -18,17 +22,22 @@ import torch  # noqa: E402
 from cwbl import abi, dist as cdist, synth  # noqa: E402
 
 args = sys.argv[1:]
-path = 1
-if args[:1] == ["--path"]:
-    path, args = int(args[1]), args[2:]
-specs = args or ["0", "12", "1", "0:16", "0:32", "0:48", "2", "3"]
-w = synth.make("c4", local_noise=True)
+path, config = 1, "c4"
+while args[:1] in (["--path"], ["--config"]):
+    if args[0] == "--path":
+        path = int(args[1])
+    else:
+        config = args[1]
+    args = args[2:]
+specs = args or (["0", "12", "1", "0:16", "0:32", "0:48", "2", "3"] if config == "c4" else
+                 ["0", "11", "13", "1", "5", "4", "2", "3"])
+w = synth.make(config, local_noise=True)
 dev = torch.device("cuda:0")
 types = [dict(family=1, type_id=w.radar_type, xyz=w.obs_xyz, obs=w.obs, hdxb=w.hdxb)]
 _, types = cdist.unpack_obs_set(torch.from_numpy(cdist.pack_obs_set(types, w.k)).to(dev))
 x, y, alt = (torch.from_numpy(a).to(dev) for a in (w.x, w.y, w.alt))
 var0 = torch.from_numpy(w.var).to(dev)
-core = abi.Core(w.k, device=0, options={"big_path": path})
+core = abi.Core(w.k, device=0, options={"big_path": path} if w.k > 64 else {})
 core.set_obs(cdist.builder_from(types, abi.MEM_DEVICE).build())
 var = var0.clone()
 slab = abi.make_slab(x, y, alt, var, memory=abi.MEM_DEVICE)
