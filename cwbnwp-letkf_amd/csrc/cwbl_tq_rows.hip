@@ -105,32 +105,17 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
     // the rows of column 4 g + kk are XOR 16 for odd kk (ColumnChunk XSW)
     const int xk = CC::xr(kk);
     const int offAx = (16 * wave + m) ^ xk, offBx = (16 * (7 - wave) + m) ^ xk;
-    int offJx[8];  // B operand of column block J
+    int offJx[NTW];
 #pragma unroll
-    for (int J = 0; J < 8; ++J) offJx[J] = (16 * J + m) ^ xk;
-    // Wave W's tiles are (W, t) for t <= W and (7 - W, t - W - 1) above: two A operands
-    // and the column blocks J = 0 .. 7 - W, each converted once per 4 columns and chosen
-    // statically (the FP64 matrix pipe and the VALU are one resource on gfx950: every VALU
-    // instruction in this loop adds to the MFMA time)
-    auto mfma_chunk = [&](auto WW, int nsl, const CC &cb) {
-      constexpr int W = decltype(WW)::value, NJ = 8 - W;
+    for (int t = 0; t < NTW; ++t) offJx[t] = (16 * (t <= wave ? t : t - wave - 1) + m) ^ xk;
+    auto chunk = [&](int nsl, const CC &cb) {
       for (int s0 = 0; s0 < (CWBL_DBG_STOP(c) == 12 ? 0 : nsl); s0 += 4) {
         const float *ys = cb.yb[s0 + kk];
         const double a = (double)ys[offAx], b = (double)ys[offBx];
-        double bj[NJ];
-        sfor<NJ>([&](auto JJ) { bj[decltype(JJ)::value] = (double)ys[offJx[decltype(JJ)::value]]; });
-        sfor<NTW>([&](auto TT) {
-          constexpr int t = decltype(TT)::value, J = t <= W ? t : t - W - 1;
-          tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(t <= W ? a : b, bj[J], tile[t], 0, 0, 0);
-        });
-      }
-    };
-    auto chunk = [&](int nsl, const CC &cb) {
-      switch (__builtin_amdgcn_readfirstlane(wave)) {  // (wave-uniform: a scalar branch)
-        case 0: mfma_chunk(std::integral_constant<int, 0>{}, nsl, cb); break;
-        case 1: mfma_chunk(std::integral_constant<int, 1>{}, nsl, cb); break;
-        case 2: mfma_chunk(std::integral_constant<int, 2>{}, nsl, cb); break;
-        default: mfma_chunk(std::integral_constant<int, 3>{}, nsl, cb); break;
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+          tile[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(t <= wave ? a : b, (double)ys[offJx[t]],
+                                                         tile[t], 0, 0, 0);
       }
       {  // Yb d: row tid % 128, the rounds of eight columns split between the two thread
          // halves (all four waves take a share), four chains
