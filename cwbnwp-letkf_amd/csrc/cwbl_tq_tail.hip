@@ -371,46 +371,75 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     y0 = fma(-c0, v0[0], fma(-c1, v0[1], fma(-c2, v0[2], fma(-c3, v0[3], y0))));
     y1 = fma(-c0, v1[0], fma(-c1, v1[1], fma(-c2, v1[2], fma(-c3, v1[3], y1))));
   };
-  // the next group's reflector entries are loaded before the current group is applied
-  auto load_tail = [&](int top, double (&v1)[4], double (&ta)[4]) {
+  // The reflector rows come from the record in HBM (a sub-batch's records are far larger than
+  // the caches): one group's loads take ~4 k cycles under load against ~350 cycles of apply4.
+  // So the groups run as a static pipeline over a ring of register slots holding the raw
+  // loaded rows only, group g + D's loads issued right after group g's rows are formed (no
+  // register copies between iterations: the wait before a group covers only its own loads,
+  // issued D groups earlier; tau, the scale and the unit entry are formed from LDS when the
+  // group is applied).  (r6: a loop that copied the next group's registers into the current
+  // ones made the compiler wait for every load at the end of each iteration — one memory
+  // latency per group.)  Groups past the last reflector (k < KP) load nothing and apply
+  // tau = 0.
+  auto issue_tail = [&](int top, double (&x)[4]) {
     sfor<4>([&](auto qq) {
       const int jl = top - 3 + qq;  // < 0: padding (H = I)
-      const int j1 = jl + 1;
-      const double xr = rec_ld(rec, rec_off(jl >= 0 && l > j1, HO::BT + jl * KT + l));
-      const double sc = sm.scl[J0 + (jl < 0 ? 0 : jl)];
-      v1[qq] = jl < 0 ? 0.0 : l == j1 ? 1.0 : (l > j1 ? sc * xr : 0.0);
-      ta[qq] = jl < 0 ? 0.0 : sm.tau[J0 + jl];
+      x[qq] = rec_ld(rec, rec_off(jl >= 0 && l > jl + 1, HO::BT + jl * KT + l));
     });
   };
-  auto load_hand = [&](int top, double (&v0)[4], double (&v1)[4], double (&ta)[4]) {
+  // (branch-free: a uniform `jl < 0 ?` select let the compiler branch around the use of the
+  // loaded row and sink the load into the branch, with a wait for it right there)
+  auto form_tail = [&](int top, const double (&x)[4], double (&v1)[4], double (&ta)[4]) {
+    sfor<4>([&](auto qq) {
+      const int jl = top - 3 + qq, jc = jl < 0 ? 0 : jl;
+      const int j1 = jl + 1;
+      const double pad = jl < 0 ? 0.0 : 1.0;  // padding group entries: H = I
+      const double sc = sm.scl[J0 + jc];
+      v1[qq] = pad * (l == j1 ? 1.0 : (l > j1 ? sc * x[qq] : 0.0));
+      ta[qq] = pad * sm.tau[J0 + jc];
+    });
+  };
+  auto issue_hand = [&](int top, double (&x0)[4], double (&x1)[4]) {
     sfor<4>([&](auto qq) {
       const int j = top - 3 + qq;
       // rows <= j hold zeros (not loaded); row j + 1 holds 1.0
-      v0[qq] = rec_ld(rec, rec_off(mem0 && l > j, HO::HV + j * KP + l));
-      v1[qq] = w[HO::HV + j * KP + J0 + l];
-      ta[qq] = sm.tau[j];
+      x0[qq] = rec_ld(rec, rec_off(mem0 && l > j, HO::HV + j * KP + l));
+      x1[qq] = w[HO::HV + j * KP + J0 + l];
     });
   };
   {
+    constexpr int NGT = (KT - 2 + 3) / 4;  // groups of this kernel's reflectors at k = KP
+    constexpr int D = NGT < 8 ? NGT : 8;   // groups in flight (8 VGPRs each)
     const double zero4[4] = {0.0, 0.0, 0.0, 0.0};
-    double v1[4], ta[4];
-    load_tail(nst - 1, v1, ta);
-    for (int top = nst - 1; top >= 0; top -= 4) {  // this kernel's reflectors: parked rows
-      double n1[4], nt[4];
-      load_tail(top - 4 >= 0 ? top - 4 : 0, n1, nt);
+    double rx[D][4];
+    sfor<D>([&](auto G) { issue_tail(nst - 1 - 4 * decltype(G)::value, rx[decltype(G)::value]); });
+    sfor<NGT>([&](auto G) {
+      constexpr int g = decltype(G)::value, sl = g % D;
+      double v1[4], ta[4];
+      form_tail(nst - 1 - 4 * g, rx[sl], v1, ta);
+      if constexpr (g + D < NGT) issue_tail(nst - 1 - 4 * (g + D), rx[sl]);
       apply4(zero4, v1, ta);
-      sfor<4>([&](auto qq) { v1[qq] = n1[qq]; ta[qq] = nt[qq]; });
-    }
+    });
   }
   {
-    double v0[4], v1[4], ta[4];
-    load_hand(J0 - 1, v0, v1, ta);
-    for (int top = J0 - 1; top >= 0; top -= 4) {  // the hand-off's reflectors (rows > j)
-      double n0[4], n1[4], nt[4];
-      load_hand(top - 4 >= 3 ? top - 4 : 3, n0, n1, nt);
+    constexpr int NGH = J0 / 4;            // the hand-off's reflectors (rows > j)
+    constexpr int D = NGH < 4 ? NGH : 4;   // (v0 and v1: 16 VGPRs each)
+    double r0[D][4], r1[D][4];
+    sfor<D>([&](auto G) {
+      constexpr int g = decltype(G)::value;
+      issue_hand(J0 - 1 - 4 * g, r0[g], r1[g]);
+    });
+    sfor<NGH>([&](auto G) {
+      constexpr int g = decltype(G)::value, sl = g % D, top = J0 - 1 - 4 * g;
+      double v0[4], v1[4], ta[4];
+      sfor<4>([&](auto qq) {
+        v0[qq] = r0[sl][qq];
+        v1[qq] = r1[sl][qq];
+        ta[qq] = sm.tau[top - 3 + decltype(qq)::value];
+      });
+      if constexpr (g + D < NGH) issue_hand(J0 - 1 - 4 * (g + D), r0[sl], r1[sl]);
       apply4(v0, v1, ta);
-      sfor<4>([&](auto qq) { v0[qq] = n0[qq]; v1[qq] = n1[qq]; ta[qq] = nt[qq]; });
-    }
+    });
   }
 
   // ---- analysis and RTPP / RTPS (:671-698), fp32 in the reference's order -----------------
