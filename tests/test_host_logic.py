@@ -135,6 +135,33 @@ def test_roofline_block_takes_the_dominant_kernel_and_its_algorithmic_flops():
     assert bench.kernel_algorithmic_flops("solve_tq_rows_kernel<128, 64>", 128, 1, 200) == a
 
 
+def test_hbm_block_sums_pmc_bytes_per_step(monkeypatch):
+    """roofline.hbm: PMC HBM bytes of every kernel x its calls / the profiled steps, over the
+    live ms_per_step and 8 TB/s; the unique-bytes figure is 4 (2k + 3) B per point."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    pmc = {"_meta": {"steps": 2},
+           "assemble_record_kernel<4>": {"hbm_bytes_per_launch": 3e9, "calls": 4},
+           "solve_tq40_kernel<40, 0>": {"hbm_bytes_per_launch": 1e9, "calls": 4},
+           "notes": "not a kernel"}
+    monkeypatch.setattr(bench, "load_pmc", lambda config: (pmc, "t"))
+    h = bench.hbm_block("c2", 40, 1_000_000, 10.0)
+    assert h["pmc_bytes_per_step"] == (3e9 * 4 + 1e9 * 4) / 2
+    assert abs(h["achieved_gbs"] - 8e9 / 1e-2 / 1e9) < 1e-9
+    assert h["frac"] == h["achieved_gbs"] / bench.HBM_PEAK_GBS and bench.HBM_PEAK_GBS == 8000.0
+    assert h["unique_bytes_per_step"] == 4.0 * 83 * 1_000_000
+    assert h["by_kernel_bytes_per_step"]["assemble_record_kernel<4>"] == 6e9
+    assert set(h["by_kernel_bytes_per_step"]) == {"assemble_record_kernel<4>",
+                                                   "solve_tq40_kernel<40, 0>"}
+    monkeypatch.setattr(bench, "load_pmc", lambda config: ({}, None))
+    assert bench.hbm_block("no-such-config", 40, 1, 10.0) is None
+    # the committed profile carries C2's figures
+    monkeypatch.undo()
+    assert bench.hbm_block("c2", 40, 1_000_000, 10.0)["pmc_bytes_per_step"] > 0
+
+
 def test_baseline_process_count_follows_affinity_and_quota():
     import os
     import sys
