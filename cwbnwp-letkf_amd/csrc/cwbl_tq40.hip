@@ -33,6 +33,22 @@ namespace cwbl {
 
 namespace {
 
+#ifndef CWBL_TQ40_UG
+#define CWBL_TQ40_UG 2
+#endif
+constexpr int kUG = CWBL_TQ40_UG;  // columns per group of the rank-2 update
+#ifndef CWBL_TQ40_NA
+#define CWBL_TQ40_NA 2
+#endif
+constexpr int kNA = CWBL_TQ40_NA;
+#ifndef CWBL_TQ40_LDSLOAD
+#define CWBL_TQ40_LDSLOAD 0
+#endif  // matvec partial sums per row (column c -> sum c % kNA)
+template <int NS>
+__device__ __forceinline__ double acc_sum(const double (&pa)[kNA][NS], int r) {
+  if constexpr (kNA == 2) return pa[0][r] + pa[1][r];
+  else return (pa[0][r] + pa[1][r]) + (pa[2][r] + pa[3][r]);
+}
 
 // Sum over this lane's 16-lane row, the same value on every lane: two quad_perm stages (two
 // v_mov_b32_dpp and a v_add_f64 each: gfx950 has no 64-bit quad_perm), then the four quad
@@ -42,10 +58,17 @@ namespace {
 __device__ __forceinline__ double rsum16(double v) {
   v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
   v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
+#if CWBL_TQ40_RS
+  double s = rbcast<0>(v), t = rbcast<8>(v);
+  s = fmac_row<4>(s, v, 1.0);
+  t = fmac_row<12>(t, v, 1.0);
+  return s + t;
+#else
   double s = rbcast<0>(v);
   s = fmac_row<4>(s, v, 1.0);
   s = fmac_row<8>(s, v, 1.0);
   return fmac_row<12>(s, v, 1.0);
+#endif
 }
 
 }  // namespace
@@ -127,8 +150,79 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   // sum(xb) * nmember_inv (:671)
   const double xb_mean = (double)(seq_sum_f32(xbl) * c.nmember_inv);
 
-  // ---- A from the record (L2/MALL-resident, written just before) -----------------------------
+  // ---- A from the record ---------------------------------------------------------------------
   double A[NS][KP];  // slot rows, all columns
+  double Pb[J0];     // prefix block row l (lanes >= J0 hold row 0's copy, never used)
+  const int lp = l < J0 ? l : 0;
+  const bool pre = l < J0;
+  double uxP, ubP, ux[NS], ub[NS];
+#if CWBL_TQ40_LDSLOAD
+  // Staged through LDS: the wave copies its four records with 16-byte loads (coalesced) in
+  // two passes, rows 0 .. J0+15 (+ b1), then rows J0+16 .. KP-1, and each lane reads its
+  // entries from LDS.  Read straight from the packed record, the rows' entries are per-lane
+  // gathers that touch up to 64 cache lines per load instruction.  The shared arrays are not
+  // live yet, so they hold the staging.
+  {
+    static_assert(NS == 2, "staging passes: slot 0 and the prefix rows, then slot 1's rows");
+    constexpr int RA = J0 + 16;              // rows of pass A
+    constexpr int WA = RA * (RA + 1) / 2;    // their packed words
+    constexpr int SA = WA + KP;              // pass A words per point: rows, then b1
+    constexpr int SB = HO::U1 - WA;          // pass B words per point
+    static_assert(4 * SA * 8 <= (int)sizeof(SM) && 4 * SB * 8 <= (int)sizeof(SM) &&
+                      WA % 2 == 0 && SB % 2 == 0 && HO::U1 % 2 == 0 && HO::WORDS % 2 == 0,
+                  "tq40 record staging");
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    double *const st = reinterpret_cast<double *>(&sm);
+    const unsigned rb0 = 4u * blockIdx.x;
+    // words [w0, w0 + N0) and [w1, w1 + N1) of each of the wave's four records, to
+    // st[p * (N0 + N1) + ...], one 16-byte piece per lane and load
+    auto stage = [&](auto n0c, unsigned w0, auto n1c, unsigned w1) {
+      constexpr int N0 = decltype(n0c)::value, N1 = decltype(n1c)::value;
+      constexpr int S = N0 + N1, CP = S / 2;
+      sfor<(4 * CP + 63) / 64>([&](auto ii) {
+        const unsigned ch = (unsigned)lane + 64u * decltype(ii)::value;
+        if (4 * CP % 64 == 0 || ch < 4u * CP) {
+          const unsigned p = ch / CP, cc = ch - p * CP;
+          const unsigned gp = rb0 + p;  // past the batch: the spare record npts
+          const unsigned rec = (gp < (unsigned)npts ? gp : (unsigned)npts) * (unsigned)HO::WORDS;
+          const unsigned wd = 2 * cc < (unsigned)N0 ? w0 + 2 * cc : w1 + 2 * cc - N0;
+          const f64x2 v = *gptr(reinterpret_cast<const f64x2 *>(
+              reinterpret_cast<const char *>(ws) + (rec + wd) * 8u));
+          *reinterpret_cast<f64x2 *>(st + p * S + 2 * cc) = v;
+        }
+      });
+    };
+    stage(std::integral_constant<int, WA>{}, 0u, std::integral_constant<int, KP>{},
+          (unsigned)HO::U1);
+    __syncthreads();
+    const int t0 = J0 + l, t1 = J0 + 16 + l;
+    const double *sa = st + q * SA;
+    sfor<RA>([&](auto cc) {  // slot 0, columns < RA: rows < RA either way
+      constexpr int col = decltype(cc)::value;
+      A[0][col] = sa[apk(t0, col)];
+    });
+    sfor<J0>([&](auto cc) {
+      constexpr int col = decltype(cc)::value;
+      Pb[col] = sa[apk(lp, col)];
+    });
+    ubP = pre ? sa[WA + lp] : 0.0;
+    ub[0] = sa[WA + t0];
+    ub[1] = sa[WA + t1];
+    __syncthreads();
+    stage(std::integral_constant<int, SB>{}, (unsigned)WA, std::integral_constant<int, 0>{}, 0u);
+    __syncthreads();
+    const double *sb = st + q * SB;  // packed word w >= WA at sb[w - WA]
+    sfor<KP - RA>([&](auto cc) {  // slot 0, columns >= RA: A(col, t0), row col >= RA
+      constexpr int col = RA + decltype(cc)::value;
+      A[0][col] = sb[apk(t0, col) - WA];
+    });
+    sfor<KP>([&](auto cc) {  // slot 1: rows t1 >= RA, and A(col, t1) has col > t1
+      constexpr int col = decltype(cc)::value;
+      A[1][col] = sb[apk(t1, col) - WA];
+    });
+    __syncthreads();  // the staging is dead before phase 1 writes the shared arrays
+  }
+#else
   sfor<NS>([&](auto rr) {
     constexpr int r = decltype(rr)::value;
     const int t = J0 + l + 16 * r;
@@ -137,24 +231,23 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       A[r][col] = w(HO::TA + apk(t, col));
     });
   });
-  double Pb[J0];  // prefix block row l (lanes >= J0 hold row 0's copy, never used)
-  const int lp = l < J0 ? l : 0;
-  const bool pre = l < J0;
   sfor<J0>([&](auto cc) {
     constexpr int col = decltype(cc)::value;
     Pb[col] = w(HO::TA + apk(lp, col));
   });
-  // x' (fp64, :671-672) and b1 = Yb d; both become Q^T x', Q^T b1
-  double uxP, ubP, ux[NS], ub[NS];
   {
     const double b = w(HO::U1 + lp);
     ubP = pre ? b : 0.0;
-    uxP = pre && l < k ? (double)xbl[0] - xb_mean : 0.0;
   }
+#endif
+  // x' (fp64, :671-672) and b1 = Yb d; both become Q^T x', Q^T b1
+  uxP = pre && l < k ? (double)xbl[0] - xb_mean : 0.0;
   sfor<NS>([&](auto rr) {
     constexpr int r = decltype(rr)::value;
     const int t = J0 + l + 16 * r;
+#if !CWBL_TQ40_LDSLOAD
     ub[r] = w(HO::U1 + t);
+#endif
     ux[r] = t < k ? (double)xbl[r + 1] - xb_mean : 0.0;
   });
 
@@ -257,16 +350,16 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     sfor<NS>([&](auto rr) { dpp_pin(v[decltype(rr)::value]); });
     // A v: slot rows over columns j+1 .. KP-1; prefix rows = their block part + the column
     // sums over the slot rows (A(i, c) = A(c, i) for c >= J0)
-    double p0[NS], p1[NS], pP = 0.0;
-    sfor<NS>([&](auto rr) { p0[decltype(rr)::value] = p1[decltype(rr)::value] = 0.0; });
+    double pa[kNA][NS], pP = 0.0;
+    sfor<kNA * NS>([&](auto ii) { pa[decltype(ii)::value / NS][decltype(ii)::value % NS] = 0.0; });
     sfor<KP - J1>([&](auto cc) {
       constexpr int col = J1 + decltype(cc)::value;
       constexpr int LC = lane_of(col);
       const double &vs = src_of(std::integral_constant<int, col>{}, vP, v);
       sfor<NS>([&](auto rr) {
         constexpr int r = decltype(rr)::value;
-        if constexpr ((col - J1) % 2 == 0) p0[r] = fmac_row<LC>(p0[r], vs, A[r][col]);
-        else p1[r] = fmac_row<LC>(p1[r], vs, A[r][col]);
+        constexpr int a = (col - J1) % kNA;
+        pa[a][r] = fmac_row<LC>(pa[a][r], vs, A[r][col]);
       });
       if constexpr (col < J0) pP = fmac_row<LC>(pP, vs, Pb[col]);
     });
@@ -283,7 +376,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     double pp[NS], sp = vP * pP;  // rows <= j: v = 0
     sfor<NS>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
-      pp[r] = p0[r] + p1[r];
+      pp[r] = acc_sum(pa, r);
       sp = fma(v[r], pp[r], sp);
     });
     const double s1 = tau * rsum16(sp);  // v^T (tau A v)
@@ -299,17 +392,31 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     double wPp = wP;
     dpp_pin(wPp);
     sfor<NS>([&](auto rr) { dpp_pin(wv[decltype(rr)::value]); });
-    sfor<KP - J1>([&](auto cc) {
-      constexpr int col = J1 + decltype(cc)::value;
-      constexpr int LC = lane_of(col);
-      const double &vs = src_of(std::integral_constant<int, col>{}, vP, v);
-      const double &ws = src_of(std::integral_constant<int, col>{}, wPp, wv);
-      sfor<NS>([&](auto rr) {
-        constexpr int r = decltype(rr)::value;
-        // A - wv v_c - v w_c, in this order
-        A[r][col] = fnmac_row<LC>(fnmac_row<LC>(A[r][col], vs, wv[r]), ws, v[r]);
+    // Columns go in pairs, each pair's first products before its second ones, so that no
+    // fmac reads the accumulator the fmac just before it wrote (the compiler puts an s_nop
+    // between two inline-asm statements that share a register)
+    sfor<(KP - J1 + kUG - 1) / kUG>([&](auto pp) {
+      constexpr int c0 = J1 + kUG * decltype(pp)::value;
+      sfor<2>([&](auto hh) {  // hh = 0: A - wv v_c; hh = 1: - v w_c (the reference's order)
+        constexpr int h = decltype(hh)::value;
+        sfor<kUG>([&](auto ee) {
+          constexpr int col = c0 + decltype(ee)::value;
+          if constexpr (col < KP) {
+            constexpr int LC = lane_of(col);
+            const double &vs = src_of(std::integral_constant<int, col>{}, vP, v);
+            const double &ws = src_of(std::integral_constant<int, col>{}, wPp, wv);
+            sfor<NS>([&](auto rr) {
+              constexpr int r = decltype(rr)::value;
+              if constexpr (h == 0) A[r][col] = fnmac_row<LC>(A[r][col], vs, wv[r]);
+              else A[r][col] = fnmac_row<LC>(A[r][col], ws, v[r]);
+            });
+            if constexpr (col < J0) {
+              if constexpr (h == 0) Pb[col] = fnmac_row<LC>(Pb[col], vs, wPp);
+              else Pb[col] = fnmac_row<LC>(Pb[col], ws, vP);
+            }
+          }
+        });
       });
-      if constexpr (col < J0) Pb[col] = fnmac_row<LC>(fnmac_row<LC>(Pb[col], vs, wPp), ws, vP);
     });
   });
   // a (one-wave) workgroup barrier: a fence the scheduler does not move phase 2 across
@@ -373,23 +480,23 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       });
       // A v over the trailing columns (v vanishes at columns <= j), column by column so
       // that one broadcast v_c is live at a time
-      double p0[NS], p1[NS];
-      sfor<NS>([&](auto rr) { p0[decltype(rr)::value] = p1[decltype(rr)::value] = 0.0; });
+      double pa[kNA][NS];
+      sfor<kNA * NS>([&](auto ii) { pa[decltype(ii)::value / NS][decltype(ii)::value % NS] = 0.0; });
       sfor<NS>([&](auto rr) { dpp_pin(v[decltype(rr)::value]); });
       sfor<KT - J1>([&](auto cc) {
         constexpr int cl = J1 + decltype(cc)::value;
         sfor<NS>([&](auto rr) {
           constexpr int r = decltype(rr)::value;
           if constexpr (16 * r + 15 > jl) {
-            if constexpr ((cl - J1) % 2 == 0) p0[r] = fmac_row<cl % 16>(p0[r], v[cl / 16], A[r][J0 + cl]);
-            else p1[r] = fmac_row<cl % 16>(p1[r], v[cl / 16], A[r][J0 + cl]);
+            constexpr int a = (cl - J1) % kNA;
+            pa[a][r] = fmac_row<cl % 16>(pa[a][r], v[cl / 16], A[r][J0 + cl]);
           }
         });
       });
       double pp[NS], sp = 0.0;
       sfor<NS>([&](auto rr) {
         constexpr int r = decltype(rr)::value;
-        pp[r] = p0[r] + p1[r];
+        pp[r] = acc_sum(pa, r);
         if constexpr (16 * r + 15 > jl) sp = fma(v[r], pp[r], sp);  // rows <= j: v = 0
       });
       const double s1 = tau * rsum16(sp);  // v^T (tau A v)
@@ -401,13 +508,25 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       });
       // A <- A - v w^T - w v^T on the trailing rows and columns
       sfor<NS>([&](auto rr) { dpp_pin(wv[decltype(rr)::value]); });
-      sfor<KT - J1>([&](auto cc) {
-        constexpr int cl = J1 + decltype(cc)::value;
-        sfor<NS>([&](auto rr) {
-          constexpr int r = decltype(rr)::value;
-          if constexpr (16 * r + 15 > jl)
-            A[r][J0 + cl] =
-                fnmac_row<cl % 16>(fnmac_row<cl % 16>(A[r][J0 + cl], v[cl / 16], wv[r]), wv[cl / 16], v[r]);
+      // column pairs, first products before second ones (as in phase 1)
+      sfor<(KT - J1 + kUG - 1) / kUG>([&](auto pp) {
+        constexpr int c0 = J1 + kUG * decltype(pp)::value;
+        sfor<2>([&](auto hh) {
+          constexpr int h = decltype(hh)::value;
+          sfor<kUG>([&](auto ee) {
+            constexpr int cl = c0 + decltype(ee)::value;
+            if constexpr (cl < KT) {
+              sfor<NS>([&](auto rr) {
+                constexpr int r = decltype(rr)::value;
+                if constexpr (16 * r + 15 > jl) {
+                  if constexpr (h == 0)
+                    A[r][J0 + cl] = fnmac_row<cl % 16>(A[r][J0 + cl], v[cl / 16], wv[r]);
+                  else
+                    A[r][J0 + cl] = fnmac_row<cl % 16>(A[r][J0 + cl], wv[cl / 16], v[r]);
+                }
+              });
+            }
+          });
         });
       });
     } else {  // the trailing 2x2: already tridiagonal (c(KP-2,KP-3) is step KP-3's beta)
