@@ -34,13 +34,16 @@ namespace cwbl {
 namespace {
 
 #ifndef CWBL_TQ40_UG
-#define CWBL_TQ40_UG 2
+#define CWBL_TQ40_UG 8
 #endif
 constexpr int kUG = CWBL_TQ40_UG;  // columns per group of the rank-2 update
 #ifndef CWBL_TQ40_NA
 #define CWBL_TQ40_NA 2
 #endif
 constexpr int kNA = CWBL_TQ40_NA;
+#ifndef CWBL_TQ40_XMV
+#define CWBL_TQ40_XMV 0
+#endif
 #ifndef CWBL_TQ40_LDSLOAD
 #define CWBL_TQ40_LDSLOAD 0
 #endif  // matvec partial sums per row (column c -> sum c % kNA)
@@ -125,15 +128,6 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     P = ii + (long long)slab.nx * (jj + (long long)slab.ny * kz);
   }
 
-  // ---- background of the point: member i = row i --------------------------------------------
-  float xbl[NV];
-  sfor<NV>([&](auto vv) {
-    constexpr int vs = decltype(vv)::value;
-    const int i = vrow(vs);
-    const bool mem = valid && i < k;
-    const float xv = slab.var[P + slab.L * (mem ? i : 0)];  // branch-free: a valid address
-    xbl[vs] = mem ? xv : 0.0f;
-  });
   // fp32 sum over members in member order; member m is row m: prefix slot lane m (m < J0),
   // else row slot (m - J0) / 16, lane (m - J0) % 16.  Every caller's x is +0 on the rows past
   // k, and s + 0 = s (s is never -0), so the rows past k need no mask and each term is one
@@ -147,8 +141,23 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     });
     return s;
   };
+  // ---- background of the point: member i = row i --------------------------------------------
+  float xbl[NV];
+  double xb_mean;
+  auto background = [&]() {
+  sfor<NV>([&](auto vv) {
+    constexpr int vs = decltype(vv)::value;
+    const int i = vrow(vs);
+    const bool mem = valid && i < k;
+    const float xv = slab.var[P + slab.L * (mem ? i : 0)];  // branch-free: a valid address
+    xbl[vs] = mem ? xv : 0.0f;
+  });
   // sum(xb) * nmember_inv (:671)
-  const double xb_mean = (double)(seq_sum_f32(xbl) * c.nmember_inv);
+  xb_mean = (double)(seq_sum_f32(xbl) * c.nmember_inv);
+  };
+#if !CWBL_TQ40_LDSLOAD
+  background();
+#endif
 
   // ---- A from the record ---------------------------------------------------------------------
   double A[NS][KP];  // slot rows, all columns
@@ -176,24 +185,42 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     const unsigned rb0 = 4u * blockIdx.x;
     // words [w0, w0 + N0) and [w1, w1 + N1) of each of the wave's four records, to
     // st[p * (N0 + N1) + ...], one 16-byte piece per lane and load
-    auto stage = [&](auto n0c, unsigned w0, auto n1c, unsigned w1) {
-      constexpr int N0 = decltype(n0c)::value, N1 = decltype(n1c)::value;
-      constexpr int S = N0 + N1, CP = S / 2;
+    // one 16-byte piece per lane and load: words [w0, w0 + N0) and [w1, w1 + N1) of each of
+    // the wave's four records; both passes' loads are issued before either is stored, so
+    // that the wave waits for memory once
+    auto load = [&](auto n0c, unsigned w0, auto n1c, unsigned w1, auto &buf) {
+      constexpr int N0 = decltype(n0c)::value, CP = (N0 + decltype(n1c)::value) / 2;
       sfor<(4 * CP + 63) / 64>([&](auto ii) {
-        const unsigned ch = (unsigned)lane + 64u * decltype(ii)::value;
-        if (4 * CP % 64 == 0 || ch < 4u * CP) {
-          const unsigned p = ch / CP, cc = ch - p * CP;
-          const unsigned gp = rb0 + p;  // past the batch: the spare record npts
-          const unsigned rec = (gp < (unsigned)npts ? gp : (unsigned)npts) * (unsigned)HO::WORDS;
-          const unsigned wd = 2 * cc < (unsigned)N0 ? w0 + 2 * cc : w1 + 2 * cc - N0;
-          const f64x2 v = *gptr(reinterpret_cast<const f64x2 *>(
-              reinterpret_cast<const char *>(ws) + (rec + wd) * 8u));
-          *reinterpret_cast<f64x2 *>(st + p * S + 2 * cc) = v;
-        }
+        // pieces past the four records re-read the last one (the store skips them)
+        const unsigned ch = min((unsigned)lane + 64u * decltype(ii)::value, 4u * CP - 1u);
+        const unsigned p = ch / CP, cc = ch - p * CP;
+        const unsigned gp = rb0 + p;  // past the batch: the spare record npts
+        const unsigned rec = (gp < (unsigned)npts ? gp : (unsigned)npts) * (unsigned)HO::WORDS;
+        const unsigned wd = 2 * cc < (unsigned)N0 ? w0 + 2 * cc : w1 + 2 * cc - N0;
+        buf[decltype(ii)::value] = *gptr(reinterpret_cast<const f64x2 *>(
+            reinterpret_cast<const char *>(ws) + (rec + wd) * 8u));
       });
     };
-    stage(std::integral_constant<int, WA>{}, 0u, std::integral_constant<int, KP>{},
-          (unsigned)HO::U1);
+    auto store = [&](auto n0c, auto n1c, const auto &buf) {
+      constexpr int S = decltype(n0c)::value + decltype(n1c)::value, CP = S / 2;
+      // pieces past the four records land past the staging (unconditional: a guarded store
+      // lets the compiler sink its load into the branch, behind a wait for every load)
+      static_assert((4 * CP + 63) / 64 * 64 * 16 <= (int)sizeof(SM), "staging overrun");
+      sfor<(4 * CP + 63) / 64>([&](auto ii) {
+        const unsigned ch = (unsigned)lane + 64u * decltype(ii)::value;
+        const unsigned p = ch / CP, cc = ch - p * CP;
+        *reinterpret_cast<f64x2 *>(st + p * S + 2 * cc) = buf[decltype(ii)::value];
+      });
+    };
+    using NA_ = std::integral_constant<int, WA>;
+    using NK_ = std::integral_constant<int, KP>;
+    using NB_ = std::integral_constant<int, SB>;
+    using N0_ = std::integral_constant<int, 0>;
+    f64x2 bufA[(4 * SA / 2 + 63) / 64], bufB[(4 * SB / 2 + 63) / 64];
+    load(NA_{}, 0u, NK_{}, (unsigned)HO::U1, bufA);
+    load(NB_{}, (unsigned)WA, N0_{}, 0u, bufB);
+    background();  // its loads behind the record's
+    store(NA_{}, NK_{}, bufA);
     __syncthreads();
     const int t0 = J0 + l, t1 = J0 + 16 + l;
     const double *sa = st + q * SA;
@@ -209,7 +236,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     ub[0] = sa[WA + t0];
     ub[1] = sa[WA + t1];
     __syncthreads();
-    stage(std::integral_constant<int, SB>{}, (unsigned)WA, std::integral_constant<int, 0>{}, 0u);
+    store(NB_{}, N0_{}, bufB);
     __syncthreads();
     const double *sb = st + q * SB;  // packed word w >= WA at sb[w - WA]
     sfor<KP - RA>([&](auto cc) {  // slot 0, columns >= RA: A(col, t0), row col >= RA
@@ -264,7 +291,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   }
   // dlarfg with fp64 rcp/rsq refined to ~1 ulp; H = I when x = 0 (tau = 0, v = e_j+1)
   struct Refl {
-    double beta, tau, scal;
+    double beta, tau, scal, amb;  // amb = alpha - beta = 1 / scal (0 when H = I)
   };
   auto dlarfg = [](double alpha, double xx) {
     const double a2 = fma(alpha, alpha, xx);
@@ -276,6 +303,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     h.tau = nz ? (bt - alpha) * -copysign(rs, alpha) : 0.0;
     const double rab = rcp64(alpha - bt);
     h.scal = nz ? rab : 0.0;
+    h.amb = nz ? alpha - bt : 0.0;
     return h;
   };
 
@@ -309,6 +337,37 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     xx = rsum16(xx);
     xu = rsum16(xu);
     xb = rsum16(xb);
+    // x_c of column c, wave-uniform per row: prefix lane c (c < J0) or its slot lane; the
+    // products with it are one fmac_row each (acc + x_c y)
+    auto src_of = [&](auto cc, const double &vp, const double (&vs)[NS]) -> const double & {
+      constexpr int col = decltype(cc)::value;
+      if constexpr (col < J0) return vp;
+      else return vs[(col - J0) / 16];
+    };
+    auto lane_of = [](int col) { return col < J0 ? col : (col - J0) % 16; };
+#if CWBL_TQ40_XMV
+    // A v = scal (A x + (alpha - beta) A(:, j+1)) on the slot rows and the prefix block's
+    // part of the prefix rows (phase 2's form): the products with x overlap the reductions
+    // and dlarfg
+    double pa[kNA][NS], pP = 0.0;
+    sfor<kNA * NS>([&](auto ii) { pa[decltype(ii)::value / NS][decltype(ii)::value % NS] = 0.0; });
+    {
+      double xPp = xP;
+      dpp_pin(xPp);
+      sfor<NS>([&](auto rr) { dpp_pin(x[decltype(rr)::value]); });
+      sfor<KP - J1 - 1>([&](auto cc) {
+        constexpr int col = J1 + 1 + decltype(cc)::value;
+        constexpr int LC = lane_of(col);
+        const double &xs = src_of(std::integral_constant<int, col>{}, xPp, x);
+        sfor<NS>([&](auto rr) {
+          constexpr int r = decltype(rr)::value;
+          constexpr int a = (col - J1 - 1) % kNA;
+          pa[a][r] = fmac_row<LC>(pa[a][r], xs, A[r][col]);
+        });
+        if constexpr (col < J0) pP = fmac_row<LC>(pP, xs, Pb[col]);
+      });
+    }
+#endif
     const Refl h = dlarfg(alpha, xx);
     // every lane of the row writes the same value (no divergent branch in the step)
     sm.tq[q][j][0] = dj;
@@ -338,16 +397,16 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       ux[r] = fma(-tau * s2, v[r], ux[r]);
       ub[r] = fma(-tau * s3, v[r], ub[r]);
     });
-    // v_c of column c, wave-uniform per row: prefix lane c (c < J0) or its slot lane; the
-    // products with it are one fmac_row each (acc + v_c y)
-    auto src_of = [&](auto cc, const double &vp, const double (&vs)[NS]) -> const double & {
-      constexpr int col = decltype(cc)::value;
-      if constexpr (col < J0) return vp;
-      else return vs[(col - J0) / 16];
-    };
-    auto lane_of = [](int col) { return col < J0 ? col : (col - J0) % 16; };
     dpp_pin(vP);
     sfor<NS>([&](auto rr) { dpp_pin(v[decltype(rr)::value]); });
+#if CWBL_TQ40_XMV
+    double pp[NS];
+    sfor<NS>([&](auto rr) {
+      constexpr int r = decltype(rr)::value;
+      pp[r] = h.scal * fma(h.amb, A[r][J1], acc_sum(pa, r));
+    });
+    if constexpr (J1 < J0) pP = h.scal * fma(h.amb, Pb[J1], pP);
+#else
     // A v: slot rows over columns j+1 .. KP-1; prefix rows = their block part + the column
     // sums over the slot rows (A(i, c) = A(c, i) for c >= J0)
     double pa[kNA][NS], pP = 0.0;
@@ -363,6 +422,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       });
       if constexpr (col < J0) pP = fmac_row<LC>(pP, vs, Pb[col]);
     });
+#endif
     sfor<J0 - J1>([&](auto cc) {  // prefix rows j+1 .. J0-1: column sums of the slots
       constexpr int col = J1 + decltype(cc)::value;
       double s = 0.0;
@@ -373,10 +433,15 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       s = rsum16(s);
       pP += l == col ? s : 0.0;
     });
-    double pp[NS], sp = vP * pP;  // rows <= j: v = 0
+#if !CWBL_TQ40_XMV
+    double pp[NS];
+#endif
+    double sp = vP * pP;  // rows <= j: v = 0
     sfor<NS>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
+#if !CWBL_TQ40_XMV
       pp[r] = acc_sum(pa, r);
+#endif
       sp = fma(v[r], pp[r], sp);
     });
     const double s1 = tau * rsum16(sp);  // v^T (tau A v)
@@ -458,6 +523,24 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       xx = rsum16(xx);
       xu = rsum16(xu);
       xb = rsum16(xb);
+#if CWBL_TQ40_XMV
+      // A v = scal (A x + (alpha - beta) A(:, j+1)) with x = column j below row j + 1: the
+      // products with x do not wait for the reflector, so they overlap its reductions and
+      // dlarfg's reciprocals
+      double pa[kNA][NS];
+      sfor<kNA * NS>([&](auto ii) { pa[decltype(ii)::value / NS][decltype(ii)::value % NS] = 0.0; });
+      sfor<NS>([&](auto rr) { dpp_pin(x[decltype(rr)::value]); });
+      sfor<KT - J1 - 1>([&](auto cc) {
+        constexpr int cl = J1 + 1 + decltype(cc)::value;
+        sfor<NS>([&](auto rr) {
+          constexpr int r = decltype(rr)::value;
+          if constexpr (16 * r + 15 > jl) {
+            constexpr int a = (cl - J1 - 1) % kNA;
+            pa[a][r] = fmac_row<cl % 16>(pa[a][r], x[cl / 16], A[r][J0 + cl]);
+          }
+        });
+      });
+#endif
       const Refl h = dlarfg(alpha, xx);
       const double tau = h.tau;
       sm.tq[q][j][0] = dj;
@@ -478,6 +561,15 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         ux[r] = fma(-tau * s2, v[r], ux[r]);
         ub[r] = fma(-tau * s3, v[r], ub[r]);
       });
+#if CWBL_TQ40_XMV
+      sfor<NS>([&](auto rr) { dpp_pin(v[decltype(rr)::value]); });
+      double pp[NS], sp = 0.0;
+      sfor<NS>([&](auto rr) {
+        constexpr int r = decltype(rr)::value;
+        pp[r] = h.scal * fma(h.amb, A[r][J0 + J1], acc_sum(pa, r));
+        if constexpr (16 * r + 15 > jl) sp = fma(v[r], pp[r], sp);  // rows <= j: v = 0
+      });
+#else
       // A v over the trailing columns (v vanishes at columns <= j), column by column so
       // that one broadcast v_c is live at a time
       double pa[kNA][NS];
@@ -499,6 +591,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         pp[r] = acc_sum(pa, r);
         if constexpr (16 * r + 15 > jl) sp = fma(v[r], pp[r], sp);  // rows <= j: v = 0
       });
+#endif
       const double s1 = tau * rsum16(sp);  // v^T (tau A v)
       double wv[NS];
       sfor<NS>([&](auto rr) {
