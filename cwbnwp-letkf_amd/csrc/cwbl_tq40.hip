@@ -41,6 +41,9 @@ constexpr int kUG = CWBL_TQ40_UG;  // columns per group of the rank-2 update
 #define CWBL_TQ40_NA 2
 #endif
 constexpr int kNA = CWBL_TQ40_NA;
+#ifndef CWBL_TQ40_WSEL
+#define CWBL_TQ40_WSEL 0
+#endif
 #ifndef CWBL_TQ40_XMV
 #define CWBL_TQ40_XMV 0
 #endif
@@ -445,7 +448,14 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       sp = fma(v[r], pp[r], sp);
     });
     const double s1 = tau * rsum16(sp);  // v^T (tau A v)
+#if CWBL_TQ40_WSEL
     const double wP = (pre && l > j) ? fma(-0.5 * tau * s1, vP, tau * pP) : 0.0;
+#else
+    // w on the rows <= j (and lanes >= J0) is not zeroed: it only updates those rows' own
+    // entries, which nothing reads again (their w is never a broadcast source: the update
+    // runs over columns > j)
+    const double wP = fma(-0.5 * tau * s1, vP, tau * pP);
+#endif
     double wv[NS];
     sfor<NS>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
@@ -597,7 +607,12 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       sfor<NS>([&](auto rr) {
         constexpr int r = decltype(rr)::value;
         const int t = l + 16 * r;
+#if CWBL_TQ40_WSEL
         wv[r] = t > jl ? fma(-0.5 * tau * s1, v[r], tau * pp[r]) : 0.0;
+#else
+        (void)t;  // rows <= j: as in phase 1
+        wv[r] = fma(-0.5 * tau * s1, v[r], tau * pp[r]);
+#endif
       });
       // A <- A - v w^T - w v^T on the trailing rows and columns
       sfor<NS>([&](auto rr) { dpp_pin(wv[decltype(rr)::value]); });
@@ -779,7 +794,11 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       constexpr int r = decltype(rr)::value;
       if constexpr (16 * r + 15 >= J1) {
         const int t = l + 16 * r;
-        vv[r] = t == J1 ? 1.0 : (t > J1 ? A[r][j] : 0.0);
+        // column j's registers hold x * scal, which is 0 on the rows <= j + 1 (x is), in the
+        // slots that step j wrote (16 r + 15 > J1): the reflector is 1 at row j + 1 and the
+        // register elsewhere
+        if constexpr (16 * r + 15 > J1) vv[r] = t == J1 ? 1.0 : A[r][j];
+        else vv[r] = t == J1 ? 1.0 : 0.0;
         a = fma(vv[r], y[r + 1], a);
       } else {
         vv[r] = 0.0;
