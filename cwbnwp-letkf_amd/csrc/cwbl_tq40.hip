@@ -41,6 +41,9 @@ constexpr int kUG = CWBL_TQ40_UG;  // columns per group of the rank-2 update
 #define CWBL_TQ40_NA 2
 #endif
 constexpr int kNA = CWBL_TQ40_NA;
+#ifndef CWBL_TQ40_RS3
+#define CWBL_TQ40_RS3 1
+#endif
 #ifndef CWBL_TQ40_WSEL
 #define CWBL_TQ40_WSEL 0
 #endif
@@ -75,6 +78,28 @@ __device__ __forceinline__ double rsum16(double v) {
   s = fmac_row<8>(s, v, 1.0);
   return fmac_row<12>(s, v, 1.0);
 #endif
+}
+
+// Three row sums, stage by stage: each stage's DPP reads come three instructions after the
+// adds that feed them, so no wait states are needed between the stages (the same sums, the
+// same rounding order as rsum16)
+__device__ __forceinline__ void rsum16x3(double &a, double &b, double &c) {
+  a += dpp_f64<0xB1>(a);
+  b += dpp_f64<0xB1>(b);
+  c += dpp_f64<0xB1>(c);
+  a += dpp_f64<0x4E>(a);
+  b += dpp_f64<0x4E>(b);
+  c += dpp_f64<0x4E>(c);
+  double sa = rbcast<0>(a), sb = rbcast<0>(b), sc = rbcast<0>(c);
+  sa = fmac_row<4>(sa, a, 1.0);
+  sb = fmac_row<4>(sb, b, 1.0);
+  sc = fmac_row<4>(sc, c, 1.0);
+  sa = fmac_row<8>(sa, a, 1.0);
+  sb = fmac_row<8>(sb, b, 1.0);
+  sc = fmac_row<8>(sc, c, 1.0);
+  a = fmac_row<12>(sa, a, 1.0);
+  b = fmac_row<12>(sb, b, 1.0);
+  c = fmac_row<12>(sc, c, 1.0);
 }
 
 }  // namespace
@@ -337,9 +362,13 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       xu = fma(x[r], ux[r], xu);
       xb = fma(x[r], ub[r], xb);
     });
+#if CWBL_TQ40_RS3
+    rsum16x3(xx, xu, xb);
+#else
     xx = rsum16(xx);
     xu = rsum16(xu);
     xb = rsum16(xb);
+#endif
     // x_c of column c, wave-uniform per row: prefix lane c (c < J0) or its slot lane; the
     // products with it are one fmac_row each (acc + x_c y)
     auto src_of = [&](auto cc, const double &vp, const double (&vs)[NS]) -> const double & {
@@ -530,9 +559,13 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
           x[r] = 0.0;
         }
       });
+#if CWBL_TQ40_RS3
+      rsum16x3(xx, xu, xb);
+#else
       xx = rsum16(xx);
       xu = rsum16(xu);
       xb = rsum16(xb);
+#endif
 #if CWBL_TQ40_XMV
       // A v = scal (A x + (alpha - beta) A(:, j+1)) with x = column j below row j + 1: the
       // products with x do not wait for the reflector, so they overlap its reductions and
