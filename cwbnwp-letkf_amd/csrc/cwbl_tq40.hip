@@ -278,18 +278,39 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     __syncthreads();  // the staging is dead before phase 1 writes the shared arrays
   }
 #else
+  // A(t, col) of row t = J0 + l + 16 r: packed word tri(t) + col where col <= t, tri(col) + t
+  // above.  A column at or left of the slot's first row is in the lower part on every lane, one
+  // right of its last row in the upper part: one lane base plus a compile-time offset each;
+  // only the columns inside the slot's row range pick per lane.
+  // Loads through a buffer resource on the wave's four records (a lane past the batch reads
+  // the spare record npts, at most three records on): the compile-time part of each offset
+  // goes in the instruction's offset fields, not in a per-load address computation.
+  const __amdgpu_buffer_rsrc_t rs = rec_rsrc(ws + (size_t)(4 * blockIdx.x) * HO::WORDS, 4 * HO::WORDS);
+  const unsigned rq = (unsigned)(valid ? q : npts - 4 * (int)blockIdx.x) * (unsigned)HO::WORDS;
+  auto rw = [&](unsigned vword, unsigned cword) {  // record word vword + cword (cword static)
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(8u * vword), (int)(8u * cword), 0);
+    return __longlong_as_double(((long long)v[1] << 32) | (unsigned)v[0]);
+  };
   sfor<NS>([&](auto rr) {
     constexpr int r = decltype(rr)::value;
-    const int t = J0 + l + 16 * r;
+    constexpr int T0 = J0 + 16 * r, T1 = T0 + 15;  // the slot's rows
+    const int t = T0 + l;
+    const unsigned lo = rq + (unsigned)(HO::TA + t * (t + 1) / 2), up = rq + (unsigned)(HO::TA + t);
     sfor<KP>([&](auto cc) {
       constexpr int col = decltype(cc)::value;
-      A[r][col] = w(HO::TA + apk(t, col));
+      constexpr unsigned tc = (unsigned)(col * (col + 1) / 2);
+      if constexpr (col <= T0) A[r][col] = rw(lo, col);
+      else if constexpr (col > T1) A[r][col] = rw(up, tc);
+      else A[r][col] = rw(col <= t ? lo + col : up + tc, 0u);
     });
   });
-  sfor<J0>([&](auto cc) {
-    constexpr int col = decltype(cc)::value;
-    Pb[col] = w(HO::TA + apk(lp, col));
-  });
+  {
+    const unsigned lo = rq + (unsigned)(HO::TA + lp * (lp + 1) / 2), up = rq + (unsigned)(HO::TA + lp);
+    sfor<J0>([&](auto cc) {
+      constexpr int col = decltype(cc)::value;
+      Pb[col] = rw(col <= lp ? lo + col : up + (unsigned)(col * (col + 1) / 2), 0u);
+    });
+  }
   {
     const double b = w(HO::U1 + lp);
     ubP = pre ? b : 0.0;
