@@ -23,7 +23,7 @@
 // After J0 steps the trailing (KP-J0)^2 matrix is held as 16-lane rows (phase 2).  Phase 1's
 // reflectors go to LDS as they are formed; phase 2's stay in the registers of the column
 // they eliminated.  Nothing is written to global memory but the analysis, and the kernel
-// spills no registers (243 VGPRs, two waves per SIMD, 19.4 KB of LDS per wave).  Every loop
+// spills no registers (244 VGPRs, two waves per SIMD, 19.4 KB of LDS per wave).  Every loop
 // over steps, slots and columns is compile-time (sfor), so all register indices are static.
 #include "cwbl_device.h"
 
@@ -33,30 +33,16 @@ namespace cwbl {
 
 namespace {
 
-#ifndef CWBL_TQ40_UG
-#define CWBL_TQ40_UG 8
-#endif
-constexpr int kUG = CWBL_TQ40_UG;  // columns per group of the rank-2 update
-#ifndef CWBL_TQ40_NA
-#define CWBL_TQ40_NA 2
-#endif
-constexpr int kNA = CWBL_TQ40_NA;
-#ifndef CWBL_TQ40_RS3
-#define CWBL_TQ40_RS3 1
-#endif
-#ifndef CWBL_TQ40_WSEL
-#define CWBL_TQ40_WSEL 0
-#endif
-#ifndef CWBL_TQ40_XMV
-#define CWBL_TQ40_XMV 0
-#endif
-#ifndef CWBL_TQ40_LDSLOAD
-#define CWBL_TQ40_LDSLOAD 0
-#endif  // matvec partial sums per row (column c -> sum c % kNA)
+// Rank-2 updates run in groups of kUG columns, each group's first products before its second
+// ones, so no fused FMA reads the accumulator the one before it wrote (the compiler puts an
+// s_nop between two inline-asm statements that share a register); the matvec keeps kNA
+// partial sums per row (column c -> sum c % kNA).  r6 A/B of the alternatives:
+// profiles/r6_tq40_ab.txt.
+constexpr int kUG = 8;
+constexpr int kNA = 2;
 template <int NS>
 __device__ __forceinline__ double acc_sum(const double (&pa)[kNA][NS], int r) {
-  if constexpr (kNA == 2) return pa[0][r] + pa[1][r];
-  else return (pa[0][r] + pa[1][r]) + (pa[2][r] + pa[3][r]);
+  return pa[0][r] + pa[1][r];
 }
 
 // Sum over this lane's 16-lane row, the same value on every lane: two quad_perm stages (two
@@ -67,17 +53,10 @@ __device__ __forceinline__ double acc_sum(const double (&pa)[kNA][NS], int r) {
 __device__ __forceinline__ double rsum16(double v) {
   v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
   v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
-#if CWBL_TQ40_RS
-  double s = rbcast<0>(v), t = rbcast<8>(v);
-  s = fmac_row<4>(s, v, 1.0);
-  t = fmac_row<12>(t, v, 1.0);
-  return s + t;
-#else
   double s = rbcast<0>(v);
   s = fmac_row<4>(s, v, 1.0);
   s = fmac_row<8>(s, v, 1.0);
   return fmac_row<12>(s, v, 1.0);
-#endif
 }
 
 // Three row sums, stage by stage: each stage's DPP reads come three instructions after the
@@ -172,20 +151,17 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   // ---- background of the point: member i = row i --------------------------------------------
   float xbl[NV];
   double xb_mean;
-  auto background = [&]() {
-  sfor<NV>([&](auto vv) {
-    constexpr int vs = decltype(vv)::value;
-    const int i = vrow(vs);
-    const bool mem = valid && i < k;
-    const float xv = slab.var[P + slab.L * (mem ? i : 0)];  // branch-free: a valid address
-    xbl[vs] = mem ? xv : 0.0f;
-  });
-  // sum(xb) * nmember_inv (:671)
-  xb_mean = (double)(seq_sum_f32(xbl) * c.nmember_inv);
-  };
-#if !CWBL_TQ40_LDSLOAD
-  background();
-#endif
+  {
+    sfor<NV>([&](auto vv) {
+      constexpr int vs = decltype(vv)::value;
+      const int i = vrow(vs);
+      const bool mem = valid && i < k;
+      const float xv = slab.var[P + slab.L * (mem ? i : 0)];  // branch-free: a valid address
+      xbl[vs] = mem ? xv : 0.0f;
+    });
+    // sum(xb) * nmember_inv (:671)
+    xb_mean = (double)(seq_sum_f32(xbl) * c.nmember_inv);
+  }
 
   // ---- A from the record ---------------------------------------------------------------------
   double A[NS][KP];  // slot rows, all columns
@@ -193,98 +169,15 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   const int lp = l < J0 ? l : 0;
   const bool pre = l < J0;
   double uxP, ubP, ux[NS], ub[NS];
-#if CWBL_TQ40_LDSLOAD
-  // Staged through LDS: the wave copies its four records with 16-byte loads (coalesced) in
-  // two passes, rows 0 .. J0+15 (+ b1), then rows J0+16 .. KP-1, and each lane reads its
-  // entries from LDS.  Read straight from the packed record, the rows' entries are per-lane
-  // gathers that touch up to 64 cache lines per load instruction.  The shared arrays are not
-  // live yet, so they hold the staging.
-  {
-    static_assert(NS == 2, "staging passes: slot 0 and the prefix rows, then slot 1's rows");
-    constexpr int RA = J0 + 16;              // rows of pass A
-    constexpr int WA = RA * (RA + 1) / 2;    // their packed words
-    constexpr int SA = WA + KP;              // pass A words per point: rows, then b1
-    constexpr int SB = HO::U1 - WA;          // pass B words per point
-    static_assert(4 * SA * 8 <= (int)sizeof(SM) && 4 * SB * 8 <= (int)sizeof(SM) &&
-                      WA % 2 == 0 && SB % 2 == 0 && HO::U1 % 2 == 0 && HO::WORDS % 2 == 0,
-                  "tq40 record staging");
-    typedef double f64x2 __attribute__((ext_vector_type(2)));
-    double *const st = reinterpret_cast<double *>(&sm);
-    const unsigned rb0 = 4u * blockIdx.x;
-    // words [w0, w0 + N0) and [w1, w1 + N1) of each of the wave's four records, to
-    // st[p * (N0 + N1) + ...], one 16-byte piece per lane and load
-    // one 16-byte piece per lane and load: words [w0, w0 + N0) and [w1, w1 + N1) of each of
-    // the wave's four records; both passes' loads are issued before either is stored, so
-    // that the wave waits for memory once
-    auto load = [&](auto n0c, unsigned w0, auto n1c, unsigned w1, auto &buf) {
-      constexpr int N0 = decltype(n0c)::value, CP = (N0 + decltype(n1c)::value) / 2;
-      sfor<(4 * CP + 63) / 64>([&](auto ii) {
-        // pieces past the four records re-read the last one (the store skips them)
-        const unsigned ch = min((unsigned)lane + 64u * decltype(ii)::value, 4u * CP - 1u);
-        const unsigned p = ch / CP, cc = ch - p * CP;
-        const unsigned gp = rb0 + p;  // past the batch: the spare record npts
-        const unsigned rec = (gp < (unsigned)npts ? gp : (unsigned)npts) * (unsigned)HO::WORDS;
-        const unsigned wd = 2 * cc < (unsigned)N0 ? w0 + 2 * cc : w1 + 2 * cc - N0;
-        buf[decltype(ii)::value] = *gptr(reinterpret_cast<const f64x2 *>(
-            reinterpret_cast<const char *>(ws) + (rec + wd) * 8u));
-      });
-    };
-    auto store = [&](auto n0c, auto n1c, const auto &buf) {
-      constexpr int S = decltype(n0c)::value + decltype(n1c)::value, CP = S / 2;
-      // pieces past the four records land past the staging (unconditional: a guarded store
-      // lets the compiler sink its load into the branch, behind a wait for every load)
-      static_assert((4 * CP + 63) / 64 * 64 * 16 <= (int)sizeof(SM), "staging overrun");
-      sfor<(4 * CP + 63) / 64>([&](auto ii) {
-        const unsigned ch = (unsigned)lane + 64u * decltype(ii)::value;
-        const unsigned p = ch / CP, cc = ch - p * CP;
-        *reinterpret_cast<f64x2 *>(st + p * S + 2 * cc) = buf[decltype(ii)::value];
-      });
-    };
-    using NA_ = std::integral_constant<int, WA>;
-    using NK_ = std::integral_constant<int, KP>;
-    using NB_ = std::integral_constant<int, SB>;
-    using N0_ = std::integral_constant<int, 0>;
-    f64x2 bufA[(4 * SA / 2 + 63) / 64], bufB[(4 * SB / 2 + 63) / 64];
-    load(NA_{}, 0u, NK_{}, (unsigned)HO::U1, bufA);
-    load(NB_{}, (unsigned)WA, N0_{}, 0u, bufB);
-    background();  // its loads behind the record's
-    store(NA_{}, NK_{}, bufA);
-    __syncthreads();
-    const int t0 = J0 + l, t1 = J0 + 16 + l;
-    const double *sa = st + q * SA;
-    sfor<RA>([&](auto cc) {  // slot 0, columns < RA: rows < RA either way
-      constexpr int col = decltype(cc)::value;
-      A[0][col] = sa[apk(t0, col)];
-    });
-    sfor<J0>([&](auto cc) {
-      constexpr int col = decltype(cc)::value;
-      Pb[col] = sa[apk(lp, col)];
-    });
-    ubP = pre ? sa[WA + lp] : 0.0;
-    ub[0] = sa[WA + t0];
-    ub[1] = sa[WA + t1];
-    __syncthreads();
-    store(NB_{}, N0_{}, bufB);
-    __syncthreads();
-    const double *sb = st + q * SB;  // packed word w >= WA at sb[w - WA]
-    sfor<KP - RA>([&](auto cc) {  // slot 0, columns >= RA: A(col, t0), row col >= RA
-      constexpr int col = RA + decltype(cc)::value;
-      A[0][col] = sb[apk(t0, col) - WA];
-    });
-    sfor<KP>([&](auto cc) {  // slot 1: rows t1 >= RA, and A(col, t1) has col > t1
-      constexpr int col = decltype(cc)::value;
-      A[1][col] = sb[apk(t1, col) - WA];
-    });
-    __syncthreads();  // the staging is dead before phase 1 writes the shared arrays
-  }
-#else
   // A(t, col) of row t = J0 + l + 16 r: packed word tri(t) + col where col <= t, tri(col) + t
   // above.  A column at or left of the slot's first row is in the lower part on every lane, one
-  // right of its last row in the upper part: one lane base plus a compile-time offset each;
-  // only the columns inside the slot's row range pick per lane.
-  // Loads through a buffer resource on the wave's four records (a lane past the batch reads
-  // the spare record npts, at most three records on): the compile-time part of each offset
-  // goes in the instruction's offset fields, not in a per-load address computation.
+  // right of its last row in the upper part: one lane base plus a compile-time offset each,
+  // and only the columns inside the slot's row range pick per lane.  The loads go through a
+  // buffer resource on the wave's four records (a lane past the batch reads the spare record
+  // npts, at most three records on), so the compile-time part of each offset sits in the
+  // instruction's offset fields instead of a per-load address computation.  (r6, measured and
+  // dropped: staging the records through LDS with coalesced 16-byte loads — equal at best,
+  // the per-lane gathers cost latency, not address throughput.)
   const __amdgpu_buffer_rsrc_t rs = rec_rsrc(ws + (size_t)(4 * blockIdx.x) * HO::WORDS, 4 * HO::WORDS);
   const unsigned rq = (unsigned)(valid ? q : npts - 4 * (int)blockIdx.x) * (unsigned)HO::WORDS;
   auto rw = [&](unsigned vword, unsigned cword) {  // record word vword + cword (cword static)
@@ -315,15 +208,12 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     const double b = w(HO::U1 + lp);
     ubP = pre ? b : 0.0;
   }
-#endif
   // x' (fp64, :671-672) and b1 = Yb d; both become Q^T x', Q^T b1
   uxP = pre && l < k ? (double)xbl[0] - xb_mean : 0.0;
   sfor<NS>([&](auto rr) {
     constexpr int r = decltype(rr)::value;
     const int t = J0 + l + 16 * r;
-#if !CWBL_TQ40_LDSLOAD
     ub[r] = w(HO::U1 + t);
-#endif
     ux[r] = t < k ? (double)xbl[r + 1] - xb_mean : 0.0;
   });
 
@@ -340,7 +230,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   }
   // dlarfg with fp64 rcp/rsq refined to ~1 ulp; H = I when x = 0 (tau = 0, v = e_j+1)
   struct Refl {
-    double beta, tau, scal, amb;  // amb = alpha - beta = 1 / scal (0 when H = I)
+    double beta, tau, scal;
   };
   auto dlarfg = [](double alpha, double xx) {
     const double a2 = fma(alpha, alpha, xx);
@@ -352,7 +242,6 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     h.tau = nz ? (bt - alpha) * -copysign(rs, alpha) : 0.0;
     const double rab = rcp64(alpha - bt);
     h.scal = nz ? rab : 0.0;
-    h.amb = nz ? alpha - bt : 0.0;
     return h;
   };
 
@@ -383,13 +272,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       xu = fma(x[r], ux[r], xu);
       xb = fma(x[r], ub[r], xb);
     });
-#if CWBL_TQ40_RS3
     rsum16x3(xx, xu, xb);
-#else
-    xx = rsum16(xx);
-    xu = rsum16(xu);
-    xb = rsum16(xb);
-#endif
     // x_c of column c, wave-uniform per row: prefix lane c (c < J0) or its slot lane; the
     // products with it are one fmac_row each (acc + x_c y)
     auto src_of = [&](auto cc, const double &vp, const double (&vs)[NS]) -> const double & {
@@ -398,29 +281,6 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       else return vs[(col - J0) / 16];
     };
     auto lane_of = [](int col) { return col < J0 ? col : (col - J0) % 16; };
-#if CWBL_TQ40_XMV
-    // A v = scal (A x + (alpha - beta) A(:, j+1)) on the slot rows and the prefix block's
-    // part of the prefix rows (phase 2's form): the products with x overlap the reductions
-    // and dlarfg
-    double pa[kNA][NS], pP = 0.0;
-    sfor<kNA * NS>([&](auto ii) { pa[decltype(ii)::value / NS][decltype(ii)::value % NS] = 0.0; });
-    {
-      double xPp = xP;
-      dpp_pin(xPp);
-      sfor<NS>([&](auto rr) { dpp_pin(x[decltype(rr)::value]); });
-      sfor<KP - J1 - 1>([&](auto cc) {
-        constexpr int col = J1 + 1 + decltype(cc)::value;
-        constexpr int LC = lane_of(col);
-        const double &xs = src_of(std::integral_constant<int, col>{}, xPp, x);
-        sfor<NS>([&](auto rr) {
-          constexpr int r = decltype(rr)::value;
-          constexpr int a = (col - J1 - 1) % kNA;
-          pa[a][r] = fmac_row<LC>(pa[a][r], xs, A[r][col]);
-        });
-        if constexpr (col < J0) pP = fmac_row<LC>(pP, xs, Pb[col]);
-      });
-    }
-#endif
     const Refl h = dlarfg(alpha, xx);
     // every lane of the row writes the same value (no divergent branch in the step)
     sm.tq[q][j][0] = dj;
@@ -452,14 +312,6 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     });
     dpp_pin(vP);
     sfor<NS>([&](auto rr) { dpp_pin(v[decltype(rr)::value]); });
-#if CWBL_TQ40_XMV
-    double pp[NS];
-    sfor<NS>([&](auto rr) {
-      constexpr int r = decltype(rr)::value;
-      pp[r] = h.scal * fma(h.amb, A[r][J1], acc_sum(pa, r));
-    });
-    if constexpr (J1 < J0) pP = h.scal * fma(h.amb, Pb[J1], pP);
-#else
     // A v: slot rows over columns j+1 .. KP-1; prefix rows = their block part + the column
     // sums over the slot rows (A(i, c) = A(c, i) for c >= J0)
     double pa[kNA][NS], pP = 0.0;
@@ -475,7 +327,6 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       });
       if constexpr (col < J0) pP = fmac_row<LC>(pP, vs, Pb[col]);
     });
-#endif
     sfor<J0 - J1>([&](auto cc) {  // prefix rows j+1 .. J0-1: column sums of the slots
       constexpr int col = J1 + decltype(cc)::value;
       double s = 0.0;
@@ -486,26 +337,18 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       s = rsum16(s);
       pP += l == col ? s : 0.0;
     });
-#if !CWBL_TQ40_XMV
     double pp[NS];
-#endif
     double sp = vP * pP;  // rows <= j: v = 0
     sfor<NS>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
-#if !CWBL_TQ40_XMV
       pp[r] = acc_sum(pa, r);
-#endif
       sp = fma(v[r], pp[r], sp);
     });
     const double s1 = tau * rsum16(sp);  // v^T (tau A v)
-#if CWBL_TQ40_WSEL
-    const double wP = (pre && l > j) ? fma(-0.5 * tau * s1, vP, tau * pP) : 0.0;
-#else
     // w on the rows <= j (and lanes >= J0) is not zeroed: it only updates those rows' own
     // entries, which nothing reads again (their w is never a broadcast source: the update
     // runs over columns > j)
     const double wP = fma(-0.5 * tau * s1, vP, tau * pP);
-#endif
     double wv[NS];
     sfor<NS>([&](auto rr) {
       constexpr int r = decltype(rr)::value;
@@ -580,31 +423,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
           x[r] = 0.0;
         }
       });
-#if CWBL_TQ40_RS3
       rsum16x3(xx, xu, xb);
-#else
-      xx = rsum16(xx);
-      xu = rsum16(xu);
-      xb = rsum16(xb);
-#endif
-#if CWBL_TQ40_XMV
-      // A v = scal (A x + (alpha - beta) A(:, j+1)) with x = column j below row j + 1: the
-      // products with x do not wait for the reflector, so they overlap its reductions and
-      // dlarfg's reciprocals
-      double pa[kNA][NS];
-      sfor<kNA * NS>([&](auto ii) { pa[decltype(ii)::value / NS][decltype(ii)::value % NS] = 0.0; });
-      sfor<NS>([&](auto rr) { dpp_pin(x[decltype(rr)::value]); });
-      sfor<KT - J1 - 1>([&](auto cc) {
-        constexpr int cl = J1 + 1 + decltype(cc)::value;
-        sfor<NS>([&](auto rr) {
-          constexpr int r = decltype(rr)::value;
-          if constexpr (16 * r + 15 > jl) {
-            constexpr int a = (cl - J1 - 1) % kNA;
-            pa[a][r] = fmac_row<cl % 16>(pa[a][r], x[cl / 16], A[r][J0 + cl]);
-          }
-        });
-      });
-#endif
       const Refl h = dlarfg(alpha, xx);
       const double tau = h.tau;
       sm.tq[q][j][0] = dj;
@@ -625,15 +444,6 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         ux[r] = fma(-tau * s2, v[r], ux[r]);
         ub[r] = fma(-tau * s3, v[r], ub[r]);
       });
-#if CWBL_TQ40_XMV
-      sfor<NS>([&](auto rr) { dpp_pin(v[decltype(rr)::value]); });
-      double pp[NS], sp = 0.0;
-      sfor<NS>([&](auto rr) {
-        constexpr int r = decltype(rr)::value;
-        pp[r] = h.scal * fma(h.amb, A[r][J0 + J1], acc_sum(pa, r));
-        if constexpr (16 * r + 15 > jl) sp = fma(v[r], pp[r], sp);  // rows <= j: v = 0
-      });
-#else
       // A v over the trailing columns (v vanishes at columns <= j), column by column so
       // that one broadcast v_c is live at a time
       double pa[kNA][NS];
@@ -655,18 +465,13 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         pp[r] = acc_sum(pa, r);
         if constexpr (16 * r + 15 > jl) sp = fma(v[r], pp[r], sp);  // rows <= j: v = 0
       });
-#endif
       const double s1 = tau * rsum16(sp);  // v^T (tau A v)
       double wv[NS];
       sfor<NS>([&](auto rr) {
         constexpr int r = decltype(rr)::value;
         const int t = l + 16 * r;
-#if CWBL_TQ40_WSEL
-        wv[r] = t > jl ? fma(-0.5 * tau * s1, v[r], tau * pp[r]) : 0.0;
-#else
         (void)t;  // rows <= j: as in phase 1
         wv[r] = fma(-0.5 * tau * s1, v[r], tau * pp[r]);
-#endif
       });
       // A <- A - v w^T - w v^T on the trailing rows and columns
       sfor<NS>([&](auto rr) { dpp_pin(wv[decltype(rr)::value]); });
