@@ -15,8 +15,12 @@ steps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 PLANS = [("default", {}),
          ("max 230k", {"max_batch": 230000}),
          ("max 320k", {"max_batch": 320000}),
-         ("max 160k lead 16", {"max_batch": 160000, "lead_div": 16}),
-         ("max 320k lead 16", {"max_batch": 320000, "lead_div": 16})]
+         ("max 128k", {"max_batch": 128000}),
+         ("max 100k", {"max_batch": 100000}),
+         ("max 64k", {"max_batch": 64000}),
+         ("max 160k lead 16", {"max_batch": 160000, "lead_div": 16})]
+if os.environ.get("PLANS"):  # a subset by index, e.g. PLANS=0,3,4
+    PLANS = [PLANS[int(i)] for i in os.environ["PLANS"].split(",")]
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 for rep in range(reps):
