@@ -206,15 +206,16 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     const double amb = nz ? alpha - bt : 0.0;
     double R[4], W[4];
     rep4(l > j1 ? x : l == j1 ? amb : 0.0, R);
-    // A v = scal * sum_{c >= j+1} A(:, c) xt_c, eight chains (volatile forms in this order: a
-    // chain's FMAs eight instructions apart, past the DPP read-after-write wait states)
-    double q[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    // A v = scal * sum_{c >= j+1} A(:, c) xt_c (volatile forms, in this order)
+    // (four chains, each chain's FMAs four instructions apart, past the DPP read-after-write
+    // wait states; r6: eight chains cost eight zeroing moves and four adds more per step,
+    // 4.45 against 4.38 ms per launch)
+    double q[4] = {0.0, 0.0, 0.0, 0.0};
     sfor<KT - 8 * gb>([&](auto cc) {
       constexpr int col = 8 * gb + decltype(cc)::value;
-      q[col % 8] = fmac_row_v<col % 16>(q[col % 8], R[col / 16], A[col]);
+      q[col % 4] = fmac_row_v<col % 16>(q[col % 4], R[col / 16], A[col]);
     });
-    const double av =
-        scal * (((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7])));  // (A v)_l
+    const double av = scal * ((q[0] + q[1]) + (q[2] + q[3]));  // (A v)_l
     const double s1 = tau * wave_sum_dpp(v * av);   // v^T (tau A v); v = 0 at rows <= j
     const double wl = l > jl ? fma(-0.5 * tau * s1, v, tau * av) : 0.0;
     const double wsl = wl * scal;
