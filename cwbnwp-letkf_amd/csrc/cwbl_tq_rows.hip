@@ -291,14 +291,17 @@ solve_tq_rows_kernel(const TreeDesc *__restrict__ trees, SolveConsts c, SlabDev 
     ux = fma(-tau * su, v, ux);
     ub = fma(-tau * sb, v, ub);
     const double hs = -0.5 * tau * s1t;
-    const double wl = r > j ? fma(hs, v, tau * (sm.p[0][r] + sm.p[1][r])) : 0.0;
+    // w is not zeroed on the eliminated rows and columns (r, c <= j): it only moves their own
+    // entries, which nothing reads again (the matvec's R is zero there and the hand-off takes
+    // columns past 63), by an orthogonal transform, so they stay bounded
+    const double wl = fma(hs, v, tau * (sm.p[0][r] + sm.p[1][r]));
     const double wsl = wl * scal;
     double W[4];
     sfor<4>([&](auto G) {
       constexpr int g = decltype(G)::value;
       if constexpr (16 * g + 15 >= c0) {
         const int cc = gcol(hh, 16 * g + (l & 15));
-        W[g] = cc > j ? fma(hs, scal * R[g], tau * (sm.p[0][cc] + sm.p[1][cc])) : 0.0;
+        W[g] = fma(hs, scal * R[g], tau * (sm.p[0][cc] + sm.p[1][cc]));
       } else {
         W[g] = 0.0;
       }

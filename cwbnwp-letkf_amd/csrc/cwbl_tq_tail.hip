@@ -217,7 +217,9 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
     });
     const double av = scal * ((q[0] + q[1]) + (q[2] + q[3]));  // (A v)_l
     const double s1 = tau * wave_sum_dpp(v * av);   // v^T (tau A v); v = 0 at rows <= j
-    const double wl = l > jl ? fma(-0.5 * tau * s1, v, tau * av) : 0.0;
+    // (w is not zeroed on the eliminated rows: as in the hand-off kernel, it only moves their
+    // own entries, which nothing reads again)
+    const double wl = fma(-0.5 * tau * s1, v, tau * av);
     const double wsl = wl * scal;
     rep4(wl, W);
     // A <- A - w v^T - v w^T, a group's eight columns per pass (each column's second FMA

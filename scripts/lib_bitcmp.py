@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Bitwise comparison of two library builds on one C2-shaped case (a kernel change that should
-leave every result bit unchanged): python scripts/lib_bitcmp.py OUT.npy [nx]  analyses one
+leave every result bit unchanged): python scripts/lib_bitcmp.py OUT.npy [nx] [config]  analyses one
 variable with the library CWBL_LIBRARY names and saves the slab; --cmp A.npy B.npy compares."""
 import os
 import sys
@@ -19,7 +19,8 @@ if sys.argv[1] == "--cmp":
 from cwbl import abi, synth  # noqa: E402
 
 nx = int(sys.argv[2]) if len(sys.argv) > 2 else 100
-w = synth.make("c2", nx=nx, ny=nx)
+cfg = sys.argv[3] if len(sys.argv) > 3 else "c2"
+w = synth.make(cfg, nx=nx, ny=nx)
 c = abi.Core(w.k, device=0)
 c.set_obs(abi.ObsSetBuilder().add_radar(w.radar_type, w.obs_xyz, w.obs, w.hdxb).build())
 var = w.var.copy()
