@@ -81,6 +81,28 @@ __device__ __forceinline__ void rsum16x3(double &a, double &b, double &c) {
   c = fmac_row<12>(sc, c, 1.0);
 }
 
+// N row sums stage by stage (rsum16x3's interleaving for the prefix rows' column sums; the
+// same rounding order as rsum16)
+template <int N>
+__device__ __forceinline__ void rsum16xN(double (&a)[N]) {
+  double s[N];
+  sfor<N>([&](auto ii) { a[decltype(ii)::value] += dpp_f64<0xB1>(a[decltype(ii)::value]); });
+  sfor<N>([&](auto ii) { a[decltype(ii)::value] += dpp_f64<0x4E>(a[decltype(ii)::value]); });
+  sfor<N>([&](auto ii) { s[decltype(ii)::value] = rbcast<0>(a[decltype(ii)::value]); });
+  sfor<N>([&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    s[i] = fmac_row<4>(s[i], a[i], 1.0);
+  });
+  sfor<N>([&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    s[i] = fmac_row<8>(s[i], a[i], 1.0);
+  });
+  sfor<N>([&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    a[i] = fmac_row<12>(s[i], a[i], 1.0);
+  });
+}
+
 }  // namespace
 
 template <int KP>
@@ -327,16 +349,29 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       });
       if constexpr (col < J0) pP = fmac_row<LC>(pP, vs, Pb[col]);
     });
-    sfor<J0 - J1>([&](auto cc) {  // prefix rows j+1 .. J0-1: column sums of the slots
-      constexpr int col = J1 + decltype(cc)::value;
-      double s = 0.0;
-      sfor<NS>([&](auto rr) {
-        constexpr int r = decltype(rr)::value;
-        s = fma(A[r][col], v[r], s);
+    if constexpr (J1 < J0) {  // prefix rows j+1 .. J0-1: column sums of the slots
+      // (in chunks of up to three: seven sums at once spill)
+      constexpr int NC = J0 - J1, CH = 3;
+      sfor<(NC + CH - 1) / CH>([&](auto kk) {
+        constexpr int c0 = J1 + CH * decltype(kk)::value;
+        constexpr int n = J0 - c0 < CH ? J0 - c0 : CH;
+        double cs[n];
+        sfor<n>([&](auto cc) {
+          constexpr int col = c0 + decltype(cc)::value;
+          double s = 0.0;
+          sfor<NS>([&](auto rr) {
+            constexpr int r = decltype(rr)::value;
+            s = fma(A[r][col], v[r], s);
+          });
+          cs[decltype(cc)::value] = s;
+        });
+        rsum16xN(cs);
+        sfor<n>([&](auto cc) {
+          constexpr int col = c0 + decltype(cc)::value;
+          pP += l == col ? cs[decltype(cc)::value] : 0.0;
+        });
       });
-      s = rsum16(s);
-      pP += l == col ? s : 0.0;
-    });
+    }
     double pp[NS];
     double sp = vP * pP;  // rows <= j: v = 0
     sfor<NS>([&](auto rr) {
