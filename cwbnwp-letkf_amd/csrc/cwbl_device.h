@@ -116,6 +116,11 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
   const int x = b & 7, l = b >> 3, q = n >> 3, r = n & 7;
   return x * q + (x < r ? x : r) + l;
 }
+// the same chunks, each walked from its end
+__device__ __forceinline__ int xcd_remap_rev(int b, int n) {
+  const int x = b & 7, l = b >> 3, q = n >> 3, r = n & 7;
+  return x * q + (x < r ? x : r) + (q + (x < r ? 1 : 0) - 1 - l);
+}
 
 __device__ __forceinline__ double wave_sum_f64(double v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -133,7 +133,10 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   __shared__ SM sm;
 
   const int lane = threadIdx.x, q = lane >> 4, l = lane & 15;
-  const int gi = 4 * blockIdx.x + q;
+  // Groups of four points, XCD by XCD like the assembly's points (xcd_remap), each XCD's chunk
+  // from its end: the records written last, still in the MALL, are read first
+  const int g4 = xcd_remap_rev(blockIdx.x, gridDim.x);
+  const int gi = 4 * g4 + q;
   const bool valid = gi < npts;
   const int k = c.k;
   const int ptot = valid ? info[gi].x : 0;
@@ -200,8 +203,8 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   // instruction's offset fields instead of a per-load address computation.  (r6, measured and
   // dropped: staging the records through LDS with coalesced 16-byte loads — equal at best,
   // the per-lane gathers cost latency, not address throughput.)
-  const __amdgpu_buffer_rsrc_t rs = rec_rsrc(ws + (size_t)(4 * blockIdx.x) * HO::WORDS, 4 * HO::WORDS);
-  const unsigned rq = (unsigned)(valid ? q : npts - 4 * (int)blockIdx.x) * (unsigned)HO::WORDS;
+  const __amdgpu_buffer_rsrc_t rs = rec_rsrc(ws + (size_t)(4 * g4) * HO::WORDS, 4 * HO::WORDS);
+  const unsigned rq = (unsigned)(valid ? q : npts - 4 * g4) * (unsigned)HO::WORDS;
   auto rw = [&](unsigned vword, unsigned cword) {  // record word vword + cword (cword static)
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(8u * vword), (int)(8u * cword), 0);
     return __longlong_as_double(((long long)v[1] << 32) | (unsigned)v[0]);
