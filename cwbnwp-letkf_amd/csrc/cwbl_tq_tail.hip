@@ -63,7 +63,9 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
   using SM = TailSmem<KP, J0>;
   __shared__ SM sm;
 
-  const int gi = xcd_remap(blockIdx.x, gridDim.x);  // the hand-off kernel's point of block b
+  // the hand-off kernel's XCD chunks, each from its end: the records it wrote last (still in
+  // the MALL) are read first
+  const int gi = xcd_remap_rev(blockIdx.x, gridDim.x);
   if (gi >= npts) return;
   const int l = threadIdx.x;
   const int k = c.k;
