@@ -18,7 +18,8 @@ PLANS = [("default", {}),
          ("max 128k", {"max_batch": 128000}),
          ("max 100k", {"max_batch": 100000}),
          ("max 64k", {"max_batch": 64000}),
-         ("max 160k lead 16", {"max_batch": 160000, "lead_div": 16})]
+         ("max 160k lead 16", {"max_batch": 160000, "lead_div": 16}),
+         ("max 80k", {"max_batch": 80000})]
 if os.environ.get("PLANS"):  # a subset by index, e.g. PLANS=0,3,4
     PLANS = [PLANS[int(i)] for i in os.environ["PLANS"].split(",")]
 dev = torch.device("cuda", 0)
