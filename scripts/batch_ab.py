@@ -19,7 +19,10 @@ PLANS = [("default", {}),
          ("max 100k", {"max_batch": 100000}),
          ("max 64k", {"max_batch": 64000}),
          ("max 160k lead 16", {"max_batch": 160000, "lead_div": 16}),
-         ("max 80k", {"max_batch": 80000})]
+         ("max 80k", {"max_batch": 80000}),
+         ("rec 78k", {"split40_batch": 78000}),
+         ("rec 52k", {"split40_batch": 52000}),
+         ("rec 39k", {"split40_batch": 39000})]
 if os.environ.get("PLANS"):  # a subset by index, e.g. PLANS=0,3,4
     PLANS = [PLANS[int(i)] for i in os.environ["PLANS"].split(",")]
 dev = torch.device("cuda", 0)
