@@ -325,7 +325,10 @@ search_binned_kernel(const TreeDesc *__restrict__ trees, int ntrees, int list_ca
   // point, which cuts this kernel's time by 25% at C2 and 38% at C5 but, overlapped with the
   // assembly, costs the step 1-2% at C2 through its extra issue cycles: profiles/r4k_*)
   __shared__ __attribute__((aligned(16))) int sgrp[64][4];
-  const int gi = blockIdx.x * 64 + threadIdx.x;
+  // blocks XCD chunk by chunk, each chunk from its end (xcd_remap_rev): the assembly reads the
+  // lists chunk by chunk from each chunk's start, so the lists written last (in the MALL) are
+  // read first
+  const int gi = xcd_remap_rev(blockIdx.x, gridDim.x) * 64 + threadIdx.x;
   if (gi >= npts) return;
   float px, py, pz;
   qs.at(gi, px, py, pz);
