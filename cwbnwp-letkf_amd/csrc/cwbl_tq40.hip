@@ -103,6 +103,13 @@ __device__ __forceinline__ void rsum16xN(double (&a)[N]) {
   });
 }
 
+// STOP = 6 (a timing bound; wrong results): the matvec and rank-2 update skip the 16-column
+// blocks right of a slot's rows (trailing column tc >= 16 (r + 1)), i.e. the products a
+// lower-triangle layout would not form, with nothing put in their place: what such a layout
+// could save at most, before the cross-lane exchange its transposed products need
+template <int STOP>
+constexpr bool upper_free(int r, int tc) { return STOP == 6 && tc >= 16 * (r + 1); }
+
 }  // namespace
 
 template <int KP>
@@ -348,7 +355,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       sfor<NS>([&](auto rr) {
         constexpr int r = decltype(rr)::value;
         constexpr int a = (col - J1) % kNA;
-        pa[a][r] = fmac_row<LC>(pa[a][r], vs, A[r][col]);
+        if constexpr (!upper_free<STOP>(r, col - J0)) pa[a][r] = fmac_row<LC>(pa[a][r], vs, A[r][col]);
       });
       if constexpr (col < J0) pP = fmac_row<LC>(pP, vs, Pb[col]);
     });
@@ -413,7 +420,8 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
             const double &ws = src_of(std::integral_constant<int, col>{}, wPp, wv);
             sfor<NS>([&](auto rr) {
               constexpr int r = decltype(rr)::value;
-              if constexpr (h == 0) A[r][col] = fnmac_row<LC>(A[r][col], vs, wv[r]);
+              if constexpr (upper_free<STOP>(r, col - J0)) {
+              } else if constexpr (h == 0) A[r][col] = fnmac_row<LC>(A[r][col], vs, wv[r]);
               else A[r][col] = fnmac_row<LC>(A[r][col], ws, v[r]);
             });
             if constexpr (col < J0) {
@@ -491,7 +499,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
         constexpr int cl = J1 + decltype(cc)::value;
         sfor<NS>([&](auto rr) {
           constexpr int r = decltype(rr)::value;
-          if constexpr (16 * r + 15 > jl) {
+          if constexpr (16 * r + 15 > jl && !upper_free<STOP>(r, cl)) {
             constexpr int a = (cl - J1) % kNA;
             pa[a][r] = fmac_row<cl % 16>(pa[a][r], v[cl / 16], A[r][J0 + cl]);
           }
@@ -523,7 +531,7 @@ solve_tq40_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
             if constexpr (cl < KT) {
               sfor<NS>([&](auto rr) {
                 constexpr int r = decltype(rr)::value;
-                if constexpr (16 * r + 15 > jl) {
+                if constexpr (16 * r + 15 > jl && !upper_free<STOP>(r, cl)) {
                   if constexpr (h == 0)
                     A[r][J0 + cl] = fnmac_row<cl % 16>(A[r][J0 + cl], v[cl / 16], wv[r]);
                   else
@@ -794,6 +802,7 @@ hipError_t launch_solve_tq40(hipStream_t s, int kp, SolveConsts c, SlabDev slab,
     case 3: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 3>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
     case 4: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 4>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
     case 5: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 5>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
+    case 6: hipLaunchKernelGGL((solve_tq40_kernel<kTq4KP, 6>), grid, dim3(64), 0, s, c, slab, g0, npts, ws, info); return hipGetLastError();
     default: break;
   }
 #endif
