@@ -238,9 +238,12 @@ solve_tqb_tail_kernel(SolveConsts c, SlabDev slab, long long g0, int npts,
       });
     });
   };
+  // (timing ablation, debug builds: CWBL_DEBUG_TQ_STOP=2 with CWBL_DEBUG_TQ_STEPS = 64 + S runs
+  // only this kernel's first S steps; the hand-off kernel's 64 all run)
+  const int nrun = CWBL_DBG_STOP(c) == 2 && CWBL_DBG_STEPS(c) > 64 ? min(nst, CWBL_DBG_STEPS(c) - 64) : nst;
   sfor<NG>([&](auto GB) {  // block gb: steps jl = 8 gb - 1 .. 8 gb + 6 (column j + 1 in group gb)
     constexpr int gb = decltype(GB)::value;
-    const int hi = min(8 * gb + 6, nst - 1);
+    const int hi = min(8 * gb + 6, nrun - 1);
     for (int jl = gb == 0 ? 0 : 8 * gb - 1; jl <= hi; ++jl) step(GB, jl);
   });
   {  // the trailing 2x2 (rows k-2, k-1): already tridiagonal
