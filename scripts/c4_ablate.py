@@ -4,7 +4,8 @@ cwbnwp-letkf_amd debuglib`, loaded with CWBL_LIBRARY=cwbnwp-letkf_amd/lib_dbg/li
 release library ignores the variables.
 
   --path 1 (hand-off path; hand-off kernel: 12 column staging only, 1 assembly only, 0:S the
-            first S of its 64 steps; tail kernel: 2 its steps only, 3 steps + quadrature)
+            first S of its 64 steps; tail kernel: 2 its steps only, 3 steps + quadrature,
+            2:64+S all hand-off steps and only the tail's first S steps)
 
   --config c2 (the record path: assembly kernel 11 = staging only (no MFMA groups), 13 =
             without the gathers, 1 = no record write; solve_tq40_kernel 5 = record loads
